@@ -1,0 +1,30 @@
+# Builds libtic.so (gfx950 HIP kernels + C-ABI runtime) in-tree so it travels with the
+# repo snapshot to the GPU box.  `make -j8` here cross-compiles without a GPU.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CSRC     := tf_image_compression_amd/csrc
+BUILD    := build
+LIB      := tf_image_compression_amd/libtic.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)
+KERNELS  := conv_s1 conv_s2 conv_t2 conv_rgb
+OBJS     := $(addprefix $(BUILD)/,$(addsuffix .o,$(KERNELS))) $(BUILD)/tic_runtime.o
+HDRS     := $(wildcard $(CSRC)/*.h) include/tic.h
+
+all: $(LIB)
+
+$(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/tic_runtime.o: $(CSRC)/tic_runtime.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-rpath,/opt/rocm/lib
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,129 @@
+/*
+ * tic.h — C-ABI of libtic.so, the MI355X (gfx950) encode/decode hot path of the
+ * learned image codec in bolin-chen/tf_image_compression.
+ *
+ * The reference has no FFI: its hot path is a TF-1.x graph built by
+ * model_N.encoder/decoder and run by tf.Session.  Each entry point below names the
+ * reference interface it replaces (paths relative to the reference root).  All
+ * arguments are plain pointers and sizes; tensors are C-contiguous NHWC.  Every
+ * function returns 0 on success or a negative TIC_E* code; tic_last_error()
+ * returns a thread-local message for the last failure on the calling thread.
+ *
+ * Host pointers (tic_encode / tic_decode / tic_rmbe) are owned by the caller and are
+ * only read/written during the call.  Device pointers (the *_device variants) must
+ * come from tic_device_alloc on the same handle; those calls are asynchronous on the
+ * handle's HIP stream — use tic_synchronize() before reading results.
+ */
+#ifndef TIC_H_
+#define TIC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TIC_OK 0
+#define TIC_EINVAL (-1)     /* bad argument / shape (reference: ValueError, tf.errors.InvalidArgumentError) */
+#define TIC_ENOTFOUND (-2)  /* unknown variable name (reference: Saver.restore NotFoundError) */
+#define TIC_ESTATE (-3)     /* handle not finalized / missing weights */
+#define TIC_EHIP (-4)       /* HIP runtime error */
+#define TIC_ENOMEM (-5)
+#define TIC_EUNSUPPORTED (-6)
+
+#define TIC_MODEL_RMBE 100  /* submit/2/rmbe/model.py:113 (block-effect post-filter) */
+
+typedef struct tic_handle tic_handle;
+
+/* Library / build identification. */
+const char* tic_version(void);
+const char* tic_last_error(void);
+
+/* Open a codec for model_N on HIP device `device`.
+ * Replaces: `from model_N import model` (encode.py:225-232, decode.py:280-287,
+ *   submit/encoder.py:220-223) + model_N/config.json's patch_size/quan_scale
+ *   (encode.py:129-145) + os.environ['CUDA_VISIBLE_DEVICES']=gpu (encode.py:218).
+ * model_id: 0..3 or TIC_MODEL_RMBE.  patch_size: even, >= 16 (for rmbe: 128).
+ * quan_scale: Q in [2, 256] (model_0/config.json:6). */
+int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_handle** out);
+void tic_destroy(tic_handle* h);
+
+/* Channel statistics (float32 [3]).
+ * Replaces: np.load('data_info/channel_normalization_params.npz') at model import
+ *   (model_0/model.py:18,26-28; submit/2/rmbe/model.py:25-30). */
+int tic_set_normalization(tic_handle* h, const float* mean3, const float* std3);
+
+/* One TF variable, by its scope name and TF layout: '<scope>/kernel' HWIO [3,3,Cin,Cout]
+ * for conv (basic_block/basic_block.py:30), [3,3,Cout,Cin] for conv-transpose (:53);
+ * '<scope>/bias' [Cout] (:35,:59).  Copied and repacked at tic_finalize.
+ * Replaces: tf.train.Saver().restore (utils/utils.py:84-93), one variable at a time. */
+int tic_set_param(tic_handle* h, const char* name, const float* data, const int64_t* shape, int ndim);
+
+/* Check every variable is present, repack and upload.  (Saver.restore's all-or-nothing.) */
+int tic_finalize(tic_handle* h);
+
+/* Shape of the quantised code for one patch (h, w, C).
+ * Replaces: encoded_patches[0][0].shape (encode.py:171) / get_encoded_shape (decode.py:130-140). */
+int tic_code_shape(const tic_handle* h, int* eh, int* ew, int* ec);
+
+/* Encoder: uint8 RGB patches [n,P,P,3] -> uint8 symbols [n,eh,ew,ec] in {0..Q-1}
+ * (optional float32 pre-quantiser activations [n,eh,ew,ec] for parity checks).
+ * Replaces: model.encoder(input, patch_size, quan_scale) (model_0/model.py:34-144)
+ *   + the sess.run loop (encode.py:157-165) + astype(int) (encode.py:182). */
+int tic_encode(tic_handle* h, const uint8_t* patches, int n, uint8_t* idx_out, float* preact_out);
+
+/* Decoder: uint8 symbols [n,eh,ew,ec] -> uint8 RGB [n,P,P,3] (np.around half-even of the
+ * clipped float) and/or the float32 reconstruction in [0,255] (either may be NULL).
+ * Replaces: model.decoder(input, quan_scale) (model_0/model.py:147-263) + sess.run loop
+ *   (decode.py:212-220) + np.around(...).astype(np.uint8) (decode.py:249). */
+int tic_decode(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb_out, float* f32_out);
+
+/* Block-effect post-filter network on float32 RGB windows [n,128,128,3] -> float32 (clipped).
+ * Handle must be created with TIC_MODEL_RMBE.
+ * Replaces: rmbe_model.model(patch_batch) + sess.run (submit/2/rmbe/model.py:113-197,
+ *   submit/2/rmbe/rmbe.py:28-67). */
+int tic_rmbe(tic_handle* h, const float* windows, int n, float* out);
+
+/* --- device-resident variants (benchmarks, multi-stage pipelines) --- */
+int tic_device_alloc(tic_handle* h, size_t bytes, void** dptr);
+int tic_device_free(tic_handle* h, void* dptr);
+int tic_memcpy_h2d(tic_handle* h, void* dst, const void* src, size_t bytes);
+int tic_memcpy_d2h(tic_handle* h, void* dst, const void* src, size_t bytes);
+int tic_synchronize(tic_handle* h);
+int tic_encode_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, float* d_preact);
+int tic_decode_device(tic_handle* h, const uint8_t* d_idx, int n, uint8_t* d_rgb, float* d_f32);
+/* encode then decode back-to-back on the handle's stream (the benchmark step). */
+int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, uint8_t* d_rgb);
+int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out);
+
+/* --- introspection / measurement --- */
+int tic_num_layers(const tic_handle* h);
+/* kind: 0 conv s1, 1 conv s2, 2 conv-transpose s2; act: 0 identity, 1 relu;
+ * stage: 0 encoder, 1 decoder.  name_buf receives the TF scope (NUL-terminated). */
+int tic_layer_info(const tic_handle* h, int i, char* name_buf, int name_len, int* kind, int* cin,
+                   int* cout, int* act, int* stage, int* residual);
+/* Static layer table keyed by model id (no handle, no device needed). */
+int tic_model_num_layers(int model_id);
+int tic_model_layer(int model_id, int i, char* name_buf, int name_len, int* kind, int* cin, int* cout,
+                    int* act, int* stage, int* residual);
+/* Time each layer's kernel with HIP events on the handle's stream over `iters` runs of
+ * tic_codec_device(n) (or the rmbe net); writes the mean ms per launch of layer i to
+ * ms_out[i] (size >= tic_num_layers). */
+int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float* ms_out);
+
+/* Unit-test entry: one layer on device float32 NHWC tensors.
+ * kind/act as tic_layer_info; res (nullable) is added after the activation.
+ * w is the TF-layout kernel (HWIO for conv, [3,3,Cout,Cin] for conv-T), host memory.
+ * in: [n,H,W,cin]; out: [n,Ho,Wo,cout]. */
+int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int n, int H, int W, int cin,
+                       int cout, const float* w_host, const float* b_host, const float* d_res, float* d_out);
+
+/* Device info string (name, CUs, arch) for logs. */
+int tic_device_info(tic_handle* h, char* buf, int len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TIC_H_ */

@@ -1,0 +1,172 @@
+"""GPU parity: libtic (gfx950 HIP) vs the CPU oracle on identical inputs and weights.
+
+Bars:
+* per layer: max |gpu - oracle| <= 3e-5 * max(1, max|oracle|) (fp32 MFMA vs f64-accumulated);
+* quantised symbols: bit-exact wherever the oracle's pre-activation is farther than
+  1e-5 * max|preact| from a quantiser decision threshold (SURVEY §7 "hard parts" 1);
+* reconstruction (decoder fed the SAME symbols): float max |diff| <= 2e-3 on the [0,255]
+  scale, uint8 differs by at most 1 and only where the float sits on a .5 rounding edge,
+  dataset-PSNR difference <= 0.02 dB (north_star tolerance).
+"""
+import numpy as np
+import pytest
+
+from conftest import structured_patches
+from oracle import tic_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+K_S1, K_S2, K_T2 = 0, 1, 2
+
+
+@pytest.fixture(scope="module")
+def lib_codec():
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    cache = {}
+
+    def get(model_id, P, Q=2):
+        key = (model_id, P, Q)
+        if key not in cache:
+            params = synthetic_params(model_id, seed=0)
+            cache[key] = (Codec(model_id, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=Q), params)
+        return cache[key]
+
+    yield get
+    for c, _ in cache.values():
+        c.close()
+
+
+LAYER_CASES = [
+    (K_S1, 64, 64, 1, False, 16, 16),
+    (K_S1, 64, 64, 1, True, 20, 13),
+    (K_S1, 64, 64, 0, False, 33, 17),
+    (K_S2, 16, 32, 1, False, 64, 64),
+    (K_S2, 32, 32, 1, False, 30, 22),
+    (K_S2, 32, 64, 1, False, 32, 32),
+    (K_S2, 64, 64, 1, False, 17, 15),
+    (K_T2, 64, 64, 1, False, 16, 16),
+    (K_T2, 64, 32, 1, False, 9, 13),
+    (K_T2, 32, 32, 1, False, 32, 32),
+    (K_T2, 32, 16, 1, False, 8, 8),
+    (K_T2, 64, 64, 0, False, 5, 21),
+]
+
+
+@pytest.mark.parametrize("kind,cin,cout,act,res,H,W", LAYER_CASES)
+def test_conv3x3_layer(lib_codec, kind, cin, cout, act, res, H, W):
+    codec, _ = lib_codec(0, 64)
+    r = np.random.default_rng(np.random.PCG64(kind * 1000 + cin + cout + H))
+    n = 2
+    x = r.standard_normal((n, H, W, cin)).astype(np.float32)
+    kshape = (3, 3, cout, cin) if kind == K_T2 else (3, 3, cin, cout)
+    k = (r.standard_normal(kshape) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    b = (r.standard_normal(cout) * 0.1).astype(np.float32)
+    params = {"l/kernel": k, "l/bias": b}
+    a = "relu" if act else "identity"
+    if kind == K_T2:
+        ref = o.my_conv2d_transpose(x, params, "l", a)
+    else:
+        ref = o.my_conv2d(x, params, "l", 1 if kind == K_S1 else 2, a)
+    resid = r.standard_normal(ref.shape).astype(np.float32) if res else None
+    if res:
+        ref = ref + resid
+    d_in = codec.alloc(x.nbytes)
+    d_in.upload(x)
+    d_out = codec.alloc(ref.nbytes)
+    d_res = None
+    if res:
+        d_res = codec.alloc(resid.nbytes)
+        d_res.upload(resid)
+    codec.conv3x3_device(kind, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
+    got = d_out.download(ref.shape, np.float32)
+    for buf in (d_in, d_out, d_res):
+        if buf is not None:
+            buf.free()
+    scale = max(1.0, float(np.max(np.abs(ref))))
+    err = float(np.max(np.abs(got - ref)))
+    assert err <= 3e-5 * scale, (err, scale)
+
+
+def _check_codec(codec, params, model_id, P, patches, Q=2):
+    idx, pre = codec.encode(patches, return_preact=True)
+    ref_pre, ref_idx = o.encoder(params, codec_mean(), codec_std(), patches, P, Q, model_id)
+    scale = max(1.0, float(np.max(np.abs(ref_pre))))
+    assert pre.shape == ref_pre.shape and idx.shape == ref_idx.shape
+    assert float(np.max(np.abs(pre - ref_pre))) <= 1e-4 * scale
+    margin = o.decision_margin(ref_pre, Q)
+    safe = margin > 1e-5 * scale
+    mism = int(np.count_nonzero((idx != ref_idx) & safe))
+    assert mism == 0, f"{mism} symbol mismatches outside the tie band"
+    # decoder on the GPU's own symbols, oracle on the same symbols
+    rgb, f = codec.decode(idx, return_float=True)
+    ref_f, ref_u8 = o.decoder(params, codec_mean(), codec_std(), idx, Q, model_id)
+    assert float(np.max(np.abs(f - ref_f))) <= 2e-3
+    du = np.abs(rgb.astype(np.int16) - ref_u8.astype(np.int16))
+    assert int(du.max()) <= 1
+    edge = np.abs((ref_f - np.floor(ref_f)) - 0.5) < 1e-2
+    assert int(np.count_nonzero((du > 0) & ~edge)) == 0
+    p_gpu = o.dataset_psnr([(patches[i], rgb[i]) for i in range(len(patches))])
+    p_ref = o.dataset_psnr([(patches[i], ref_u8[i]) for i in range(len(patches))])
+    assert abs(p_gpu - p_ref) <= 0.02, (p_gpu, p_ref)
+    return idx, rgb
+
+
+def codec_mean():
+    from tf_image_compression_amd.weights import SYNTH_MEAN
+    return SYNTH_MEAN
+
+
+def codec_std():
+    from tf_image_compression_amd.weights import SYNTH_STD
+    return SYNTH_STD
+
+
+@pytest.mark.parametrize("model_id", [0, 1, 2, 3])
+def test_codec_small_patches(lib_codec, model_id):
+    P = 64
+    codec, params = lib_codec(model_id, P)
+    patches = structured_patches(3, P, seed=model_id)
+    _check_codec(codec, params, model_id, P, patches)
+
+
+def test_codec_model3_native_128(lib_codec):
+    codec, params = lib_codec(3, 128)
+    patches = structured_patches(2, 128, seed=7)
+    _check_codec(codec, params, 3, 128, patches)
+
+
+def test_codec_model0_full_size(lib_codec):
+    """configs[1] geometry (256x256): oracle on 4 patches, batch invariance at n=64."""
+    P = 256
+    codec, params = lib_codec(0, P)
+    patches = structured_patches(4, P, seed=11)
+    idx4, rgb4 = _check_codec(codec, params, 0, P, patches)
+    big = np.concatenate([patches, structured_patches(60, P, seed=12)])
+    idx64 = codec.encode(big)
+    rgb64 = codec.decode(idx64)
+    assert np.array_equal(idx64[:4], idx4)
+    assert np.array_equal(rgb64[:4], rgb4)
+    # determinism
+    assert np.array_equal(codec.encode(big), idx64)
+
+
+def test_quan_scale_256(lib_codec):
+    """Q = 256 (base_model/1/config.json:6): multi-level quantiser + 256-entry LUT."""
+    P = 64
+    codec, params = lib_codec(0, P, Q=256)
+    patches = structured_patches(2, P, seed=5)
+    _check_codec(codec, params, 0, P, patches, Q=256)
+
+
+def test_rmbe_network(lib_codec):
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import RMBE_ID
+    params = synthetic_params(RMBE_ID)
+    r = np.random.default_rng(3)
+    win = np.clip(r.normal(120, 50, (3, 128, 128, 3)), 0, 255).astype(np.float32)
+    with Codec(RMBE_ID, params, SYNTH_MEAN, SYNTH_STD, patch_size=128) as c:
+        got = c.rmbe_windows(win)
+    ref = o.rmbe_model(params, SYNTH_MEAN, SYNTH_STD, win)
+    assert float(np.max(np.abs(got - ref))) <= 2e-3

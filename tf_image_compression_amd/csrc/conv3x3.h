@@ -1,0 +1,430 @@
+// conv3x3.h — gfx950 (CDNA4) kernels for the 3x3 convolution stacks of the codec.
+//
+// One implicit-GEMM template covers every layer with Cin, Cout multiples of 16:
+//   MODE_S1  tf.nn.conv2d stride 1 'SAME'       (basic_block/basic_block.py:33)
+//   MODE_S2  tf.nn.conv2d stride 2 'SAME'       (pad_before = 0, pad_after = 1 on even input)
+//   MODE_T2  tf.nn.conv2d_transpose stride 2 'SAME', output 2Hx2W (basic_block.py:54-57),
+//            computed as its four sub-pixel phases: y[2m+p] = sum_{(k,d) in T(p)} x[m+d] W[k],
+//            T(0) = {(0,0),(2,-1)}, T(1) = {(1,0)} — no zero-insertion, no wasted MACs.
+// with the epilogue of my_conv2d fused: + bias, ReLU/identity, + residual (res_block,
+// basic_block.py:91), and optionally the quantiser (model_0/model.py:136-138) writing u8
+// symbols; the dequantiser LUT (model_0/model.py:153) is fused into the input staging.
+//
+// Matrix core: v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, 64 FLOP/clk/SIMD — the fp32
+// peak of the chip).  GEMM orientation: M = 16 output channels (A = weights),
+// N = 16 output pixels along x (B = activations), K = input channels.  Each lane keeps
+// 4 consecutive output channels of one pixel -> 16-byte NHWC stores.
+//
+// K ordering: a 16-channel chunk is consumed by 4 MFMAs; lane group g = lane>>4 supplies
+// channel 4g+t to MFMA t, so ONE ds_read_b128 (activations) and ONE global_load_dwordx4
+// (weights) per lane feed four MFMAs.  Weights are repacked at load time to
+// [tap][Cin/16][Cout][4 (g)][4 (t)] so a wave's A fragment is one contiguous 1 KiB read.
+//
+// LDS: the block's input tile (with halo) is staged once, pixel stride PS = Cin + 8
+// floats (== 8 mod 16): the ds_read_b128 of 16 consecutive pixels x 4 channel groups hits
+// 16 distinct 16-byte bank slots in every lane group -> conflict-free.  Stride-2 tiles are
+// stored column-deinterleaved (even / odd planes) so a block of 16 consecutive output
+// pixels again reads 16 consecutive LDS pixels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tic_kernels.h"
+
+namespace tic {
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Quantiser: round_half_even(sigmoid(v) * (Q-1)), clamped to [0, Q-1].
+__device__ __forceinline__ uint32_t quant1(float v, float qscale) {
+  float s = 1.0f / (1.0f + expf(-v));
+  float q = rintf(__fmul_rn(s, qscale));
+  q = fminf(fmaxf(q, 0.0f), qscale);
+  return (uint32_t)q;
+}
+
+template <int MODE, int TH>
+struct TileGeom {
+  // LDS rows / entries per row of the staged input tile (TW = 16 output pixels wide)
+  static constexpr int LR = MODE == MODE_S1 ? TH + 2 : (MODE == MODE_S2 ? 2 * TH + 1 : TH + 1);
+  static constexpr int LC = MODE == MODE_S1 ? 18 : (MODE == MODE_S2 ? 34 : 17);
+};
+
+// Grid: x = ceil(Wg/16), y = ceil(Hg/TH), z = batch, where (Hg,Wg) is the output grid
+// (S1/S2) or the input grid (T2).  256 threads = 4 waves = WR row-groups x (4/WR)
+// channel-groups; each wave owns MB = TH/WR rows of 16 pixels x NB = Cout/16/(4/WR)
+// channel blocks (x 4 phases for T2).
+template <int MODE, int CIN, int COUT, int TH, int WR, int ACT, bool RES, int IN, int OUT>
+__global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
+  static_assert(CIN % 16 == 0 && COUT % 16 == 0, "channels must be multiples of 16");
+  constexpr int PS = CIN + 8;
+  constexpr int KC = CIN / 16;
+  constexpr int NBT = COUT / 16;
+  constexpr int WC = 4 / WR;
+  static_assert(WR * WC == 4 && TH % WR == 0 && NBT % WC == 0, "bad wave split");
+  constexpr int NB = NBT / WC;
+  constexpr int MB = TH / WR;
+  constexpr int NPH = MODE == MODE_T2 ? 4 : 1;
+  constexpr int LR = TileGeom<MODE, TH>::LR;
+  constexpr int LC = TileGeom<MODE, TH>::LC;
+  constexpr int C4 = CIN / 4;
+
+  __shared__ __attribute__((aligned(16))) float lds[LR * LC * PS];
+
+  const int tid = threadIdx.x;
+  const int gx0 = blockIdx.x * 16;
+  const int gy0 = blockIdx.y * TH;
+  const int nimg = blockIdx.z;
+  const int H = a.H, W = a.W;
+
+  // ---- stage the input tile (with halo) into LDS; zero outside the image (SAME pad) ----
+  for (int e = tid; e < LR * LC * C4; e += 256) {
+    const int c4 = e % C4;
+    const int pe = e / C4;
+    const int col = pe % LC;
+    const int row = pe / LC;
+    int iy, ix;
+    if constexpr (MODE == MODE_S2) {
+      const int plane = col >= 17 ? 1 : 0;
+      const int j = col - plane * 17;
+      iy = 2 * gy0 + row - a.pad_y;
+      ix = 2 * gx0 + 2 * j + plane - a.pad_x;
+    } else if constexpr (MODE == MODE_S1) {
+      iy = gy0 - a.pad_y + row;
+      ix = gx0 - a.pad_x + col;
+    } else {
+      iy = gy0 - 1 + row;
+      ix = gx0 - 1 + col;
+    }
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4;
+      if constexpr (IN == IN_F32) {
+        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
+      } else {
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
+        v.x = a.lut[q & 0xff];
+        v.y = a.lut[(q >> 8) & 0xff];
+        v.z = a.lut[(q >> 16) & 0xff];
+        v.w = a.lut[q >> 24];
+      }
+    }
+    *reinterpret_cast<f32x4*>(&lds[(row * LC + col) * PS + c4 * 4]) = v;
+  }
+  __syncthreads();
+
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wr = wave / WC;
+  const int wc = wave % WC;
+  const int li = lane & 15;  // pixel within the 16-pixel block (B col / D col)
+  const int lg = lane >> 4;  // k group (A/B) / output channel quad (D)
+
+  f32x4 acc[NPH][MB][NB];
+#pragma unroll
+  for (int p = 0; p < NPH; ++p)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* __restrict__ wp = a.wp;
+  // per-lane weight offset inside one (tap, kc) slab
+  const int wlane = ((wc * NB) * 16 + li) * 16 + lg * 4;
+
+  if constexpr (MODE != MODE_T2) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        f32x4 av[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          av[nb] = *reinterpret_cast<const f32x4*>(wp + (size_t)(tap * KC + kc) * COUT * 16 + wlane + nb * 256);
+        f32x4 bv[MB];
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const int r = wr * MB + mb;
+          int lp;
+          if constexpr (MODE == MODE_S1) lp = (r + ky) * LC + li + kx;
+          else lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
+          bv[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) acc[0][mb][nb] = mfma4(av[nb][t], bv[mb][t], acc[0][mb][nb]);
+      }
+    }
+  } else {
+    // input offsets (dy,dx) in {0,-1}^2; phase p = 2*py + px uses tap (ky,kx)
+#pragma unroll
+    for (int off = 0; off < 4; ++off) {
+      const int dy = -(off >> 1), dx = -(off & 1);
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        f32x4 bv[MB];
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const int r = wr * MB + mb;
+          const int lp = (r + 1 + dy) * LC + li + 1 + dx;
+          bv[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
+        }
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+          if (dy != 0 && py == 1) continue;
+          const int ky = py == 1 ? 1 : (dy == 0 ? 0 : 2);
+#pragma unroll
+          for (int px = 0; px < 2; ++px) {
+            if (dx != 0 && px == 1) continue;
+            const int kx = px == 1 ? 1 : (dx == 0 ? 0 : 2);
+            const int tap = ky * 3 + kx;
+            f32x4 av[NB];
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+              av[nb] = *reinterpret_cast<const f32x4*>(wp + (size_t)(tap * KC + kc) * COUT * 16 + wlane + nb * 256);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+              for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+                  acc[py * 2 + px][mb][nb] = mfma4(av[nb][t], bv[mb][t], acc[py * 2 + px][mb][nb]);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- fused epilogue: + bias, act, + residual, store f32 or quantise to u8 ----
+  const int Ho = a.Ho, Wo = a.Wo;
+#pragma unroll
+  for (int p = 0; p < NPH; ++p) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int r = wr * MB + mb;
+      int oy, ox;
+      if constexpr (MODE == MODE_T2) {
+        if (gy0 + r >= H || gx0 + li >= W) continue;
+        oy = 2 * (gy0 + r) + (p >> 1);
+        ox = 2 * (gx0 + li) + (p & 1);
+      } else {
+        oy = gy0 + r;
+        ox = gx0 + li;
+        if (oy >= Ho || ox >= Wo) continue;
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int co = (wc * NB + nb) * 16 + lg * 4;
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + co);
+        f32x4 v = acc[p][mb][nb];
+        v.x = __fadd_rn(v.x, bb.x);
+        v.y = __fadd_rn(v.y, bb.y);
+        v.z = __fadd_rn(v.z, bb.z);
+        v.w = __fadd_rn(v.w, bb.w);
+        if constexpr (ACT == ACT_RELU) {
+          v.x = fmaxf(v.x, 0.f);
+          v.y = fmaxf(v.y, 0.f);
+          v.z = fmaxf(v.z, 0.f);
+          v.w = fmaxf(v.w, 0.f);
+        }
+        const size_t o = ((size_t)(nimg * Ho + oy) * Wo + ox) * COUT + co;
+        if constexpr (RES) {
+          const f32x4 rr = *reinterpret_cast<const f32x4*>(a.res + o);
+          v.x = __fadd_rn(v.x, rr.x);
+          v.y = __fadd_rn(v.y, rr.y);
+          v.z = __fadd_rn(v.z, rr.z);
+          v.w = __fadd_rn(v.w, rr.w);
+        }
+        if constexpr (OUT == OUT_F32) {
+          *reinterpret_cast<f32x4*>(a.out + o) = v;
+        } else {
+          if (a.out) *reinterpret_cast<f32x4*>(a.out + o) = v;
+          const uint32_t q = quant1(v.x, a.qscale) | (quant1(v.y, a.qscale) << 8) |
+                             (quant1(v.z, a.qscale) << 16) | (quant1(v.w, a.qscale) << 24);
+          *reinterpret_cast<uint32_t*>(a.qout + o) = q;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// First layer: stride-2 3x3 conv from 3-channel RGB (u8 or f32) with the normalisation
+// (x - mean) / std (model_0/model.py:44) fused into the LDS staging.  K = 27 (+1 zero)
+// = 7 MFMA k-steps; lane group g supplies k = 4t + g -> (tap, channel) = divmod(k, 3).
+// Weights packed [Cout][4 (g)][8 (t, t=7 zero)].
+// ---------------------------------------------------------------------------------------
+
+template <int COUT, int TH, bool U8>
+__global__ void __launch_bounds__(256) conv_rgb_s2_kernel(const RgbInArgs a) {
+  constexpr int NBT = COUT / 16;
+  constexpr int MB = TH / 4;  // 4 waves split rows
+  constexpr int LR = 2 * TH + 1, LC = 34;
+  constexpr int PLANE = LR * LC;
+  __shared__ float lds[3 * PLANE];
+
+  const int tid = threadIdx.x;
+  const int gx0 = blockIdx.x * 16, gy0 = blockIdx.y * TH, nimg = blockIdx.z;
+  const int H = a.H, W = a.W;
+  for (int e = tid; e < PLANE; e += 256) {
+    const int col = e % LC, row = e / LC;
+    const int plane = col >= 17 ? 1 : 0;
+    const int iy = 2 * gy0 + row - a.pad_y, ix = 2 * gx0 + 2 * (col - plane * 17) + plane - a.pad_x;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      const size_t off = ((size_t)(nimg * H + iy) * W + ix) * 3;
+      float x0, x1, x2;
+      if constexpr (U8) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(a.in) + off;
+        x0 = p[0];
+        x1 = p[1];
+        x2 = p[2];
+      } else {
+        const float* p = reinterpret_cast<const float*>(a.in) + off;
+        x0 = p[0];
+        x1 = p[1];
+        x2 = p[2];
+      }
+      v0 = __fdiv_rn(__fsub_rn(x0, a.mean[0]), a.std[0]);
+      v1 = __fdiv_rn(__fsub_rn(x1, a.mean[1]), a.std[1]);
+      v2 = __fdiv_rn(__fsub_rn(x2, a.mean[2]), a.std[2]);
+    }
+    lds[e] = v0;
+    lds[PLANE + e] = v1;
+    lds[2 * PLANE + e] = v2;
+  }
+  __syncthreads();
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lg = lane >> 4;
+  f32x4 acc[MB][NBT];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NBT; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 w0[NBT], w1[NBT];
+#pragma unroll
+  for (int nb = 0; nb < NBT; ++nb) {
+    const float* wq = a.wp + ((nb * 16 + li) * 4 + lg) * 8;
+    w0[nb] = *reinterpret_cast<const f32x4*>(wq);
+    w1[nb] = *reinterpret_cast<const f32x4*>(wq + 4);
+  }
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const int k = 4 * t + lg;  // lane-dependent (tap, channel)
+    const int tap = k / 3, c = k - 3 * (k / 3);
+    const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int r = wave * MB + mb;
+      float b = 0.f;
+      if (k < 27) b = lds[c * PLANE + (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1)];
+#pragma unroll
+      for (int nb = 0; nb < NBT; ++nb) {
+        const float av = t < 4 ? w0[nb][t & 3] : w1[nb][t & 3];
+        acc[mb][nb] = mfma4(av, b, acc[mb][nb]);
+      }
+    }
+  }
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int oy = gy0 + wave * MB + mb, ox = gx0 + li;
+    if (oy >= a.Ho || ox >= a.Wo) continue;
+#pragma unroll
+    for (int nb = 0; nb < NBT; ++nb) {
+      const int co = nb * 16 + lg * 4;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + co);
+      f32x4 v = acc[mb][nb];
+      v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
+      v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
+      v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
+      v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
+      *reinterpret_cast<f32x4*>(a.out + ((size_t)(nimg * a.Ho + oy) * a.Wo + ox) * COUT + co) = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Last layer: stride-2 transpose conv Cin -> 3 (identity) with denormalise + clip
+// (model_0/model.py:250-259) and the host's np.around -> uint8 (decode.py:249) fused.
+// Dense sub-pixel GEMM: M = 16 rows = 4 phases x (3 channels + 1 pad), K = 4 input offsets
+// x Cin, N = 16 input positions; weights [off][Cin/16][16 rows][4][4] with zeros where a
+// phase does not use an offset.  Lane (li, g) ends with phase g, channels 0..2 of pixel li.
+// ---------------------------------------------------------------------------------------
+
+template <int CIN, int TH>
+__global__ void __launch_bounds__(256) convT_rgb_kernel(const RgbOutArgs a) {
+  constexpr int PS = CIN + 8, KC = CIN / 16, C4 = CIN / 4;
+  constexpr int LR = TH + 1, LC = 17;
+  constexpr int MB = TH / 4;
+  __shared__ __attribute__((aligned(16))) float lds[LR * LC * PS];
+
+  const int tid = threadIdx.x;
+  const int gx0 = blockIdx.x * 16, gy0 = blockIdx.y * TH, nimg = blockIdx.z;
+  const int H = a.H, W = a.W;
+  for (int e = tid; e < LR * LC * C4; e += 256) {
+    const int c4 = e % C4, pe = e / C4, col = pe % LC, row = pe / LC;
+    const int iy = gy0 - 1 + row, ix = gx0 - 1 + col;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+      v = *reinterpret_cast<const f32x4*>(a.in + ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4);
+    *reinterpret_cast<f32x4*>(&lds[(row * LC + col) * PS + c4 * 4]) = v;
+  }
+  __syncthreads();
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lg = lane >> 4;
+  f32x4 acc[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int off = 0; off < 4; ++off) {
+    const int dy = -(off >> 1), dx = -(off & 1);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(a.wp + ((off * KC + kc) * 16 + li) * 16 + lg * 4);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        const int r = wave * MB + mb;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(&lds[((r + 1 + dy) * LC + li + 1 + dx) * PS + kc * 16 + lg * 4]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[mb] = mfma4(av[t], bv[t], acc[mb]);
+      }
+    }
+  }
+  const int Ho = 2 * H, Wo = 2 * W;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = gy0 + wave * MB + mb, q = gx0 + li;
+    if (m >= H || q >= W) continue;
+    const int oy = 2 * m + (lg >> 1), ox = 2 * q + (lg & 1);
+    const size_t o = ((size_t)(nimg * Ho + oy) * Wo + ox) * 3;
+    float y[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = __fadd_rn(acc[mb][c], a.bias[c]);
+      float d = __fadd_rn(__fmul_rn(v, a.std[c]), a.mean[c]);
+      d = fminf(fmaxf(d, 0.f), 255.f);
+      y[c] = d;
+    }
+    if (a.out_f32) {
+      a.out_f32[o] = y[0];
+      a.out_f32[o + 1] = y[1];
+      a.out_f32[o + 2] = y[2];
+    }
+    if (a.out_u8) {
+      a.out_u8[o] = (uint8_t)rintf(y[0]);
+      a.out_u8[o + 1] = (uint8_t)rintf(y[1]);
+      a.out_u8[o + 2] = (uint8_t)rintf(y[2]);
+    }
+  }
+}
+
+}  // namespace tic

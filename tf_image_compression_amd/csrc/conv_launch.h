@@ -1,0 +1,18 @@
+// conv_launch.h — grid computation + registry helpers for conv3x3_kernel instantiations.
+#pragma once
+#include "conv3x3.h"
+
+namespace tic {
+
+template <int MODE, int CIN, int COUT, int TH, int WR, int ACT, bool RES, int IN, int OUT>
+static void launch_conv(const ConvArgs& a, int n, hipStream_t s) {
+  const int hg = MODE == MODE_T2 ? a.H : a.Ho;
+  const int wg = MODE == MODE_T2 ? a.W : a.Wo;
+  dim3 grid((wg + 15) / 16, (hg + TH - 1) / TH, n);
+  hipLaunchKernelGGL((conv3x3_kernel<MODE, CIN, COUT, TH, WR, ACT, RES, IN, OUT>), grid, dim3(256), 0, s, a);
+}
+
+}  // namespace tic
+
+#define TIC_CONV(MODE, CIN, COUT, TH, WR, ACT, RES, IN, OUT) \
+  { MODE, CIN, COUT, ACT, RES, IN, OUT, TH, &tic::launch_conv<MODE, CIN, COUT, TH, WR, ACT, RES, IN, OUT> }

@@ -1,0 +1,18 @@
+// Stride-2 'SAME' 3x3 convolutions of the analysis stacks (model_0/model.py:62-96,
+// model_2/model.py:62-122, model_3/model.py:62-161, rmbe conv_2).
+#include "conv_launch.h"
+
+namespace tic {
+static const ConvEntry kS2[] = {
+    TIC_CONV(MODE_S2, 16, 32, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_S2, 32, 32, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_S2, 32, 64, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_S2, 64, 64, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_S2, 64, 64, 4, 4, ACT_ID, false, IN_F32, OUT_QUANT),
+    TIC_CONV(MODE_S2, 64, 80, 4, 4, ACT_ID, false, IN_F32, OUT_QUANT),
+};
+const ConvEntry* conv_registry_s2(int* count) {
+  *count = sizeof(kS2) / sizeof(kS2[0]);
+  return kS2;
+}
+}  // namespace tic

@@ -1,0 +1,19 @@
+// Stride-2 'SAME' transposed 3x3 convolutions of the synthesis stacks
+// (model_0/model.py:198-234, model_2/model.py:118-180, model_3/model.py:157-286, rmbe conv_5).
+#include "conv_launch.h"
+
+namespace tic {
+static const ConvEntry kT2[] = {
+    TIC_CONV(MODE_T2, 64, 64, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_T2, 64, 32, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_T2, 32, 32, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_T2, 32, 16, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV(MODE_T2, 64, 64, 4, 4, ACT_ID, false, IN_IDX, OUT_F32),
+    TIC_CONV(MODE_T2, 80, 64, 4, 4, ACT_ID, false, IN_IDX, OUT_F32),
+    TIC_CONV(MODE_T2, 64, 64, 4, 4, ACT_ID, false, IN_F32, OUT_F32),
+};
+const ConvEntry* conv_registry_t2(int* count) {
+  *count = sizeof(kT2) / sizeof(kT2[0]);
+  return kT2;
+}
+}  // namespace tic

@@ -1,0 +1,67 @@
+// tic_kernels.h — argument blocks and the launch registry shared by the kernels
+// (conv_*.hip) and the host runtime (tic_runtime.cpp).  Internal; not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tic {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum { MODE_S1 = 0, MODE_S2 = 1, MODE_T2 = 2 };
+enum { ACT_ID = 0, ACT_RELU = 1 };
+enum { IN_F32 = 0, IN_IDX = 1 };
+enum { OUT_F32 = 0, OUT_QUANT = 1 };
+
+struct ConvArgs {
+  const void* in;      // f32 NHWC [N,H,W,Cin]  or u8 symbols (IN_IDX)
+  const float* wp;     // packed weights [tap][Cin/16][Cout][4][4]
+  const float* bias;   // [Cout]
+  const float* res;    // residual [N,Ho,Wo,Cout] or nullptr
+  float* out;          // f32 [N,Ho,Wo,Cout]; with OUT_QUANT: optional pre-activation
+  uint8_t* qout;       // OUT_QUANT: u8 symbols [N,Ho,Wo,Cout]
+  const float* lut;    // IN_IDX: dequantiser table (Q entries)
+  int H, W;            // input spatial
+  int Ho, Wo;          // output spatial
+  int pad_y, pad_x;    // SAME pad_before (S1: 1; S2: 0 for even input, 1 for odd; T2: unused)
+  float qscale;        // Q - 1
+};
+
+struct RgbInArgs {
+  const void* in;      // [N,H,W,3] u8 or f32
+  const float* wp;     // [Cout][4][8]
+  const float* bias;   // [Cout]
+  float* out;          // [N,Ho,Wo,Cout]
+  int H, W, Ho, Wo;
+  int pad_y, pad_x;    // SAME pad_before of the stride-2 conv
+  float mean[3], std[3];
+};
+
+struct RgbOutArgs {
+  const float* in;     // [N,H,W,Cin]
+  const float* wp;     // [4 off][Cin/16][16 rows][4][4]
+  const float* bias;   // [3]
+  uint8_t* out_u8;     // [N,2H,2W,3] or nullptr
+  float* out_f32;      // [N,2H,2W,3] or nullptr
+  int H, W;
+  float mean[3], std[3];
+};
+
+typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);
+
+struct ConvEntry {
+  int mode, cin, cout, act, res, in, out;
+  int th;             // output rows per block (input rows for T2)
+  ConvLaunch fn;
+};
+
+// All compiled conv3x3 variants (conv_s1.hip, conv_s2.hip, conv_t2.hip).
+const ConvEntry* conv_registry_s1(int* count);
+const ConvEntry* conv_registry_s2(int* count);
+const ConvEntry* conv_registry_t2(int* count);
+
+// First / last layer launchers (conv_rgb.hip); return false if the width is not compiled.
+bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s);
+bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s);
+
+}  // namespace tic

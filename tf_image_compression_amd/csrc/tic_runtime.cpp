@@ -1,0 +1,815 @@
+// tic_runtime.cpp — host runtime + C-ABI of libtic.so (see include/tic.h).
+//
+// Owns, per handle: the HIP device + a non-blocking stream, the model's layer table
+// (keyed by model id — the executing copy of model_N/model.py's encoder/decoder), the
+// weights repacked into the kernels' layouts, the dequantiser LUT and a 3-buffer f32
+// activation workspace sized for the batch chunk.  Encode / decode are issued as one
+// kernel per convolution on the handle's stream; nothing here synchronises except the
+// host-pointer entry points and tic_synchronize.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/tic.h"
+#include "tic_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(TIC_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                                \
+  } while (0)
+
+enum { K_S1 = 0, K_S2 = 1, K_T2 = 2 };
+
+struct LayerDef {
+  std::string name;
+  int kind, cin, cout, act, stage, residual;
+};
+
+// ---- layer tables: model_{0,1,2,3}/model.py encoder/decoder, submit/2/rmbe/model.py ----
+struct Block {
+  const char* name;
+  int kind;  // K_S1/K_S2/K_T2, or 3 = res_block
+  int cin, cout, act;
+};
+
+std::vector<LayerDef> expand(const std::vector<Block>& enc, const std::vector<Block>& dec) {
+  std::vector<LayerDef> out;
+  for (int stage = 0; stage < 2; ++stage) {
+    for (const Block& b : stage == 0 ? enc : dec) {
+      if (b.kind == 3) {  // basic_block.res_block: conv_0, conv_1 (relu), + input (:91)
+        out.push_back({std::string(b.name) + "/conv_0", K_S1, b.cin, b.cout, 1, stage, 0});
+        out.push_back({std::string(b.name) + "/conv_1", K_S1, b.cout, b.cout, 1, stage, 1});
+      } else {
+        out.push_back({b.name, b.kind, b.cin, b.cout, b.act, stage, 0});
+      }
+    }
+  }
+  return out;
+}
+
+bool model_table(int model_id, std::vector<LayerDef>* out) {
+  const int R = 1, I = 0, RES = 3;
+  if (model_id == 0 || model_id == 1) {  // model_0/model.py:50-246; model_1 widths 16
+    const int w = model_id == 0 ? 32 : 16;
+    *out = expand({{"encode_0", K_S2, 3, w, R}, {"encode_1", K_S2, w, 32, R},
+                   {"encode_2", K_S2, 32, 64, R}, {"encode_3", K_S2, 64, 64, R},
+                   {"encode_res_1", RES, 64, 64, R}, {"encode_res_2", RES, 64, 64, R},
+                   {"encode_4", K_S1, 64, 64, I}},
+                  {{"decode_4", K_S1, 64, 64, I},
+                   {"decode_res_1", RES, 64, 64, R}, {"decode_res_2", RES, 64, 64, R},
+                   {"decode_3", K_T2, 64, 64, R}, {"decode_2", K_T2, 64, 32, R},
+                   {"decode_1", K_T2, 32, w, R}, {"decode_0", K_T2, w, 3, I}});
+    return true;
+  }
+  if (model_id == 2) {  // model_2/model.py:50-193
+    *out = expand({{"encode_1", K_S2, 3, 32, R}, {"encode_2", K_S2, 32, 64, R},
+                   {"encode_3", K_S2, 64, 64, R},
+                   {"encode_res_1", RES, 64, 64, R}, {"encode_res_2", RES, 64, 64, R},
+                   {"encode_4", K_S2, 64, 64, I}},
+                  {{"decode_4", K_T2, 64, 64, I},
+                   {"decode_res_1", RES, 64, 64, R}, {"decode_res_2", RES, 64, 64, R},
+                   {"decode_3", K_T2, 64, 64, R}, {"decode_2", K_T2, 64, 32, R},
+                   {"decode_1", K_T2, 32, 3, I}});
+    return true;
+  }
+  if (model_id == 3) {  // model_3/model.py:50-300
+    *out = expand({{"encode_1", K_S2, 3, 32, R}, {"encode_2", K_S2, 32, 64, R},
+                   {"encode_res_m1", RES, 64, 64, R}, {"encode_res_0", RES, 64, 64, R},
+                   {"encode_3", K_S2, 64, 64, R},
+                   {"encode_res_1", RES, 64, 64, R}, {"encode_res_2", RES, 64, 64, R},
+                   {"encode_res_3", RES, 64, 64, R},
+                   {"encode_4", K_S2, 64, 80, I}},
+                  {{"decode_4", K_T2, 80, 64, I},
+                   {"decode_res_1", RES, 64, 64, R}, {"decode_res_2", RES, 64, 64, R},
+                   {"decode_res_3", RES, 64, 64, R},
+                   {"decode_3", K_T2, 64, 64, R},
+                   {"decode_res_4", RES, 64, 64, R}, {"decode_res_5", RES, 64, 64, R},
+                   {"decode_2", K_T2, 64, 32, R}, {"decode_1", K_T2, 32, 3, I}});
+    return true;
+  }
+  if (model_id == TIC_MODEL_RMBE) {  // submit/2/rmbe/model.py:118-189
+    *out = expand({{"conv_1", K_S2, 3, 32, R}, {"conv_2", K_S2, 32, 64, R},
+                   {"conv_3", K_S1, 64, 64, R}, {"conv_4", K_S1, 64, 64, R}},
+                  {{"conv_5", K_T2, 64, 32, R}, {"conv6", K_T2, 32, 3, I}});
+    return true;
+  }
+  return false;
+}
+
+int out_size(int kind, int h) { return kind == K_S2 ? (h + 1) / 2 : (kind == K_T2 ? 2 * h : h); }
+
+// TF 'SAME' pad_before for a 3x3 conv: max((out-1)*s + 3 - in, 0) / 2.
+int same_pad(int kind, int h) {
+  if (kind == K_T2) return 0;
+  const int s = kind == K_S2 ? 2 : 1;
+  const int o = out_size(kind, h);
+  return std::max((o - 1) * s + 3 - h, 0) / 2;
+}
+
+const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, int in, int outm) {
+  const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
+                                           tic::conv_registry_t2};
+  int n = 0;
+  const tic::ConvEntry* e = regs[mode](&n);
+  for (int i = 0; i < n; ++i)
+    if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
+        e[i].out == outm)
+      return &e[i];
+  return nullptr;
+}
+
+// Repack a TF kernel into the generic conv layout [tap][Cin/16][Cout][4 g][4 t].
+void pack_generic(const float* k, int kind, int cin, int cout, std::vector<float>* wp) {
+  const int KC = cin / 16;
+  wp->assign((size_t)9 * cin * cout, 0.f);
+  for (int tap = 0; tap < 9; ++tap)
+    for (int kc = 0; kc < KC; ++kc)
+      for (int co = 0; co < cout; ++co)
+        for (int g = 0; g < 4; ++g)
+          for (int t = 0; t < 4; ++t) {
+            const int ci = kc * 16 + 4 * g + t;
+            const float v = kind == K_T2 ? k[((size_t)tap * cout + co) * cin + ci]   // [kh,kw,Cout,Cin]
+                                         : k[((size_t)tap * cin + ci) * cout + co];  // HWIO
+            (*wp)[((((size_t)tap * KC + kc) * cout + co) * 4 + g) * 4 + t] = v;
+          }
+}
+
+// First layer: [Cout][4 g][8 t], k = 4t + g -> (tap, c) = divmod(k, 3); k = 27 -> 0.
+void pack_rgb_in(const float* k, int cout, std::vector<float>* wp) {
+  wp->assign((size_t)cout * 32, 0.f);
+  for (int co = 0; co < cout; ++co)
+    for (int g = 0; g < 4; ++g)
+      for (int t = 0; t < 7; ++t) {
+        const int kk = 4 * t + g;
+        if (kk >= 27) continue;
+        const int tap = kk / 3, c = kk % 3;
+        (*wp)[((size_t)co * 4 + g) * 8 + t] = k[((size_t)tap * 3 + c) * cout + co];
+      }
+}
+
+// Last layer (conv-T Cin -> 3): [4 off][Cin/16][16 rows = phase*4 + co][4 g][4 t].
+void pack_rgb_out(const float* k, int cin, std::vector<float>* wp) {
+  const int KC = cin / 16;
+  wp->assign((size_t)4 * cin * 16, 0.f);
+  for (int off = 0; off < 4; ++off) {
+    const int dy = -(off >> 1), dx = -(off & 1);
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      if ((dy != 0 && py == 1) || (dx != 0 && px == 1)) continue;
+      const int ky = py ? 1 : (dy == 0 ? 0 : 2);
+      const int kx = px ? 1 : (dx == 0 ? 0 : 2);
+      for (int co = 0; co < 3; ++co)
+        for (int ci = 0; ci < cin; ++ci) {
+          const int kc = ci / 16, g = (ci % 16) / 4, t = ci % 4;
+          (*wp)[((((size_t)off * KC + kc) * 16 + ph * 4 + co) * 4 + g) * 4 + t] =
+              k[(((size_t)ky * 3 + kx) * 3 + co) * cin + ci];
+        }
+    }
+  }
+}
+
+}  // namespace
+
+struct LayerRT {
+  LayerDef def;
+  std::vector<float> k, b;
+  bool has_k = false, has_b = false;
+  float* d_w = nullptr;
+  float* d_b = nullptr;
+  int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
+};
+
+struct tic_handle {
+  int model_id = 0, P = 0, Q = 2, device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<LayerRT> layers;
+  int n_enc = 0;
+  float mean[3] = {0, 0, 0}, std[3] = {1, 1, 1};
+  bool has_norm = false, finalized = false;
+  float* d_lut = nullptr;
+  int chunk = 256;
+  size_t act_elems = 0;  // max f32 activation elements per patch
+  int ws_batch = 0;
+  float* ws[3] = {nullptr, nullptr, nullptr};
+  // host-entry staging
+  void* st_in = nullptr;
+  size_t st_in_bytes = 0;
+  void* st_out = nullptr;
+  size_t st_out_bytes = 0;
+  void* st_out2 = nullptr;
+  size_t st_out2_bytes = 0;
+  std::vector<void*> user_allocs;
+  bool rmbe() const { return model_id == TIC_MODEL_RMBE; }
+};
+
+namespace {
+
+int ensure(void** p, size_t* have, size_t need) {
+  if (*have >= need) return TIC_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIP_TRY(hipMalloc(p, need));
+  *have = need;
+  return TIC_OK;
+}
+
+int ensure_ws(tic_handle* h, int n) {
+  if (h->ws_batch >= n) return TIC_OK;
+  for (auto& b : h->ws) {
+    if (b) (void)hipFree(b);
+    b = nullptr;
+  }
+  h->ws_batch = 0;
+  for (auto& b : h->ws) HIP_TRY(hipMalloc((void**)&b, h->act_elems * (size_t)n * sizeof(float)));
+  h->ws_batch = n;
+  return TIC_OK;
+}
+
+int check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(TIC_EHIP, "kernel launch failed: %s", hipGetErrorString(e));
+  return TIC_OK;
+}
+
+struct Prof {
+  hipEvent_t* ev;  // 2 per layer, or nullptr
+};
+
+// Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
+// outputs per-position flags.  Buffers rotate through h->ws.
+int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_idx, float* d_pre,
+               uint8_t* d_rgb, float* d_f32, const Prof& prof) {
+  const int L = (int)h->layers.size();
+  int cur = -1;       // ws index holding the current activation (-1: external input)
+  int block_in = -1;  // ws index of the enclosing res_block's input
+  for (int li = l0; li < l1; ++li) {
+    LayerRT& lay = h->layers[li];
+    const LayerDef& d = lay.def;
+    const bool first = li == 0;
+    const bool last = li == L - 1;
+    const bool last_enc = !h->rmbe() && li == h->n_enc - 1;
+    const bool first_dec = !h->rmbe() && li == h->n_enc;
+    // choose the output buffer: any ws not holding the input or the res-block input
+    int dst = -1;
+    for (int b = 0; b < 3; ++b)
+      if (b != cur && b != block_in) {
+        dst = b;
+        break;
+      }
+    const bool starts_block = d.kind == K_S1 && !d.residual && li + 1 < L && h->layers[li + 1].def.residual;
+    if (starts_block) block_in = cur;
+    const float* src = cur >= 0 ? h->ws[cur] : nullptr;
+    if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li], h->stream));
+    if (first) {
+      tic::RgbInArgs a{};
+      a.in = in;
+      a.wp = lay.d_w;
+      a.bias = lay.d_b;
+      a.out = h->ws[dst];
+      a.H = a.W = lay.h_in;
+      a.Ho = a.Wo = lay.h_out;
+      a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
+      for (int c = 0; c < 3; ++c) {
+        a.mean[c] = h->mean[c];
+        a.std[c] = h->std[c];
+      }
+      if (!tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, h->stream))
+        return fail(TIC_EUNSUPPORTED, "first layer %s: width %d not compiled", d.name.c_str(), d.cout);
+    } else if (last) {
+      tic::RgbOutArgs a{};
+      a.in = src;
+      a.wp = lay.d_w;
+      a.bias = lay.d_b;
+      a.out_u8 = d_rgb;
+      a.out_f32 = d_f32;
+      a.H = a.W = lay.h_in;
+      for (int c = 0; c < 3; ++c) {
+        a.mean[c] = h->mean[c];
+        a.std[c] = h->std[c];
+      }
+      if (!tic::launch_rgb_out(d.cin, a, n, h->stream))
+        return fail(TIC_EUNSUPPORTED, "last layer %s: width %d not compiled", d.name.c_str(), d.cin);
+    } else {
+      const int inm = first_dec ? tic::IN_IDX : tic::IN_F32;
+      const int outm = last_enc ? tic::OUT_QUANT : tic::OUT_F32;
+      const tic::ConvEntry* e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
+      if (!e)
+        return fail(TIC_EUNSUPPORTED, "no kernel for layer %s (kind %d %d->%d act %d res %d in %d out %d)",
+                    d.name.c_str(), d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
+      tic::ConvArgs a{};
+      a.in = first_dec ? in : (const void*)src;
+      a.wp = lay.d_w;
+      a.bias = lay.d_b;
+      a.res = d.residual ? h->ws[block_in] : nullptr;
+      a.out = last_enc ? d_pre : h->ws[dst];
+      a.qout = last_enc ? d_idx : nullptr;
+      a.lut = h->d_lut;
+      a.H = a.W = lay.h_in;
+      a.Ho = a.Wo = lay.h_out;
+      a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
+      a.qscale = (float)(h->Q - 1);
+      e->fn(a, n, h->stream);
+    }
+    int rc = check_launch();
+    if (rc) return rc;
+    if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li + 1], h->stream));
+    if (d.residual) block_in = -1;
+    cur = dst;
+  }
+  return TIC_OK;
+}
+
+int check_ready(tic_handle* h) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (!h->finalized) return fail(TIC_ESTATE, "handle not finalized (call tic_finalize after tic_set_param)");
+  HIP_TRY(hipSetDevice(h->device));
+  return TIC_OK;
+}
+
+size_t code_elems(const tic_handle* h) {
+  const LayerRT& l = h->layers[h->n_enc - 1];
+  return (size_t)l.h_out * l.h_out * l.def.cout;
+}
+
+// chunked drivers (device pointers)
+int encode_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, float* pre, const Prof& prof) {
+  const size_t in_pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
+  for (int s = 0; s < n; s += h->chunk) {
+    const int m = std::min(h->chunk, n - s);
+    int rc = ensure_ws(h, m);
+    if (rc) return rc;
+    rc = run_layers(h, 0, h->n_enc, in + s * in_pp, m, idx + s * ce, pre ? pre + s * ce : nullptr, nullptr,
+                    nullptr, prof);
+    if (rc) return rc;
+  }
+  return TIC_OK;
+}
+
+int decode_dev(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb, float* f32, const Prof& prof) {
+  const size_t out_pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
+  for (int s = 0; s < n; s += h->chunk) {
+    const int m = std::min(h->chunk, n - s);
+    int rc = ensure_ws(h, m);
+    if (rc) return rc;
+    rc = run_layers(h, h->n_enc, (int)h->layers.size(), idx + s * ce, m, nullptr, nullptr,
+                    rgb ? rgb + s * out_pp : nullptr, f32 ? f32 + s * out_pp : nullptr, prof);
+    if (rc) return rc;
+  }
+  return TIC_OK;
+}
+
+int rmbe_dev(tic_handle* h, const float* in, int n, float* out, const Prof& prof) {
+  const size_t pp = (size_t)h->P * h->P * 3;
+  for (int s = 0; s < n; s += h->chunk) {
+    const int m = std::min(h->chunk, n - s);
+    int rc = ensure_ws(h, m);
+    if (rc) return rc;
+    rc = run_layers(h, 0, (int)h->layers.size(), in + s * pp, m, nullptr, nullptr, nullptr, out + s * pp, prof);
+    if (rc) return rc;
+  }
+  return TIC_OK;
+}
+
+int fill_layer_info(const LayerDef& d, char* name_buf, int name_len, int* kind, int* cin, int* cout, int* act,
+                    int* stage, int* residual) {
+  if (name_buf && name_len > 0) {
+    std::strncpy(name_buf, d.name.c_str(), name_len - 1);
+    name_buf[name_len - 1] = 0;
+  }
+  if (kind) *kind = d.kind;
+  if (cin) *cin = d.cin;
+  if (cout) *cout = d.cout;
+  if (act) *act = d.act;
+  if (stage) *stage = d.stage;
+  if (residual) *residual = d.residual;
+  return TIC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tic_version(void) { return "tic 0.1.0 (gfx950, fp32 MFMA 16x16x4)"; }
+
+const char* tic_last_error(void) { return g_err.c_str(); }
+
+int tic_model_num_layers(int model_id) {
+  std::vector<LayerDef> t;
+  if (!model_table(model_id, &t)) return fail(TIC_EINVAL, "unknown model id %d", model_id);
+  return (int)t.size();
+}
+
+int tic_model_layer(int model_id, int i, char* name_buf, int name_len, int* kind, int* cin, int* cout, int* act,
+                    int* stage, int* residual) {
+  std::vector<LayerDef> t;
+  if (!model_table(model_id, &t)) return fail(TIC_EINVAL, "unknown model id %d", model_id);
+  if (i < 0 || i >= (int)t.size()) return fail(TIC_EINVAL, "layer index %d out of range", i);
+  return fill_layer_info(t[i], name_buf, name_len, kind, cin, cout, act, stage, residual);
+}
+
+int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_handle** out) {
+  if (!out) return fail(TIC_EINVAL, "null output handle pointer");
+  *out = nullptr;
+  std::vector<LayerDef> table;
+  if (!model_table(model_id, &table)) return fail(TIC_EINVAL, "unknown model id %d (expected 0..3 or %d)", model_id, TIC_MODEL_RMBE);
+  if (patch_size < 16 || patch_size % 2 != 0 || patch_size > 8192)
+    return fail(TIC_EINVAL, "patch_size %d must be even and in [16, 8192]", patch_size);
+  if (quan_scale < 2 || quan_scale > 256) return fail(TIC_EINVAL, "quan_scale %d must be in [2, 256]", quan_scale);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(TIC_EINVAL, "device %d not available (%d visible)", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  tic_handle* h = new tic_handle();
+  h->model_id = model_id;
+  h->P = patch_size;
+  h->Q = quan_scale;
+  h->device = device;
+  int hh = patch_size;
+  size_t act = 0;
+  for (const LayerDef& d : table) {
+    LayerRT l;
+    l.def = d;
+    l.h_in = hh;
+    l.h_out = out_size(d.kind, hh);
+    hh = l.h_out;
+    act = std::max(act, (size_t)l.h_out * l.h_out * d.cout);
+    if (d.stage == 0) h->n_enc++;
+    h->layers.push_back(std::move(l));
+  }
+  h->act_elems = act;
+  if (!table.empty() && hh != patch_size) {
+    delete h;
+    return fail(TIC_EINVAL, "patch_size %d: decoder output would be %dx%d (needs %d stride-2 halvings to stay even)",
+                patch_size, hh, hh, (int)std::count_if(table.begin(), table.end(), [](const LayerDef& d) { return d.kind == K_S2; }));
+  }
+  if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
+  hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(TIC_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = h;
+  return TIC_OK;
+}
+
+void tic_destroy(tic_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& l : h->layers) {
+    if (l.d_w) (void)hipFree(l.d_w);
+    if (l.d_b) (void)hipFree(l.d_b);
+  }
+  for (auto& b : h->ws)
+    if (b) (void)hipFree(b);
+  if (h->d_lut) (void)hipFree(h->d_lut);
+  if (h->st_in) (void)hipFree(h->st_in);
+  if (h->st_out) (void)hipFree(h->st_out);
+  if (h->st_out2) (void)hipFree(h->st_out2);
+  for (void* p : h->user_allocs) (void)hipFree(p);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int tic_set_normalization(tic_handle* h, const float* mean3, const float* std3) {
+  if (!h || !mean3 || !std3) return fail(TIC_EINVAL, "null argument");
+  for (int c = 0; c < 3; ++c) {
+    if (!(std3[c] != 0.f) || !std::isfinite(std3[c]) || !std::isfinite(mean3[c]))
+      return fail(TIC_EINVAL, "invalid normalisation statistics for channel %d", c);
+    h->mean[c] = mean3[c];
+    h->std[c] = std3[c];
+  }
+  h->has_norm = true;
+  return TIC_OK;
+}
+
+int tic_set_param(tic_handle* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  if (!h || !name || !data || (!shape && ndim > 0)) return fail(TIC_EINVAL, "null argument");
+  std::string nm(name);
+  // accept TF-style ':0' suffixes
+  if (nm.size() > 2 && nm.compare(nm.size() - 2, 2, ":0") == 0) nm.resize(nm.size() - 2);
+  const size_t slash = nm.rfind('/');
+  if (slash == std::string::npos) return fail(TIC_ENOTFOUND, "variable %s not in model %d", name, h->model_id);
+  const std::string scope = nm.substr(0, slash), leaf = nm.substr(slash + 1);
+  for (LayerRT& l : h->layers) {
+    if (l.def.name != scope) continue;
+    const LayerDef& d = l.def;
+    if (leaf == "kernel") {
+      const int64_t want[4] = {3, 3, d.kind == K_T2 ? d.cout : d.cin, d.kind == K_T2 ? d.cin : d.cout};
+      if (ndim != 4 || shape[0] != want[0] || shape[1] != want[1] || shape[2] != want[2] || shape[3] != want[3])
+        return fail(TIC_EINVAL, "%s: expected shape [3,3,%lld,%lld]", name, (long long)want[2], (long long)want[3]);
+      l.k.assign(data, data + (size_t)9 * d.cin * d.cout);
+      l.has_k = true;
+      h->finalized = false;
+      return TIC_OK;
+    }
+    if (leaf == "bias") {
+      if (ndim != 1 || shape[0] != d.cout) return fail(TIC_EINVAL, "%s: expected shape [%d]", name, d.cout);
+      l.b.assign(data, data + d.cout);
+      l.has_b = true;
+      h->finalized = false;
+      return TIC_OK;
+    }
+  }
+  return fail(TIC_ENOTFOUND, "variable %s not in model %d", name, h->model_id);
+}
+
+int tic_finalize(tic_handle* h) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (!h->has_norm) return fail(TIC_ESTATE, "normalisation statistics not set (tic_set_normalization)");
+  for (const LayerRT& l : h->layers) {
+    if (!l.has_k) return fail(TIC_ESTATE, "missing variable %s/kernel", l.def.name.c_str());
+    if (!l.has_b) return fail(TIC_ESTATE, "missing variable %s/bias", l.def.name.c_str());
+  }
+  HIP_TRY(hipSetDevice(h->device));
+  const int L = (int)h->layers.size();
+  for (int i = 0; i < L; ++i) {
+    LayerRT& l = h->layers[i];
+    std::vector<float> wp;
+    if (i == 0) pack_rgb_in(l.k.data(), l.def.cout, &wp);
+    else if (i == L - 1) pack_rgb_out(l.k.data(), l.def.cin, &wp);
+    else pack_generic(l.k.data(), l.def.kind, l.def.cin, l.def.cout, &wp);
+    if (l.d_w) (void)hipFree(l.d_w);
+    if (l.d_b) (void)hipFree(l.d_b);
+    l.d_w = l.d_b = nullptr;
+    HIP_TRY(hipMalloc((void**)&l.d_w, wp.size() * sizeof(float)));
+    HIP_TRY(hipMemcpy(l.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&l.d_b, std::max<size_t>(l.b.size(), 16) * sizeof(float)));
+    HIP_TRY(hipMemcpy(l.d_b, l.b.data(), l.b.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
+  // dequantiser LUT, float32 op for op as model_0/model.py:153 + basic_block.py:153
+  std::vector<float> lut(256, 0.f);
+  const float den = (float)((double)(h->Q - 1) + 1e-5);
+  for (int q = 0; q < h->Q; ++q) {
+    const float a = ((float)q + 1e-6f) / den;
+    lut[q] = logf(a / (1.0f - a));
+  }
+  if (!h->d_lut) HIP_TRY(hipMalloc((void**)&h->d_lut, 256 * sizeof(float)));
+  HIP_TRY(hipMemcpy(h->d_lut, lut.data(), 256 * sizeof(float), hipMemcpyHostToDevice));
+  h->finalized = true;
+  return TIC_OK;
+}
+
+int tic_code_shape(const tic_handle* h, int* eh, int* ew, int* ec) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (h->rmbe()) return fail(TIC_EINVAL, "rmbe handle has no code");
+  const LayerRT& l = h->layers[h->n_enc - 1];
+  if (eh) *eh = l.h_out;
+  if (ew) *ew = l.h_out;
+  if (ec) *ec = l.def.cout;
+  return TIC_OK;
+}
+
+int tic_device_alloc(tic_handle* h, size_t bytes, void** dptr) {
+  if (!h || !dptr) return fail(TIC_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMalloc(dptr, std::max<size_t>(bytes, 16)));
+  h->user_allocs.push_back(*dptr);
+  return TIC_OK;
+}
+
+int tic_device_free(tic_handle* h, void* dptr) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  auto it = std::find(h->user_allocs.begin(), h->user_allocs.end(), dptr);
+  if (it == h->user_allocs.end()) return fail(TIC_EINVAL, "pointer not allocated by this handle");
+  h->user_allocs.erase(it);
+  HIP_TRY(hipFree(dptr));
+  return TIC_OK;
+}
+
+int tic_memcpy_h2d(tic_handle* h, void* dst, const void* src, size_t bytes) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return TIC_OK;
+}
+
+int tic_memcpy_d2h(tic_handle* h, void* dst, const void* src, size_t bytes) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return TIC_OK;
+}
+
+int tic_synchronize(tic_handle* h) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return TIC_OK;
+}
+
+int tic_encode_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, float* d_preact) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (h->rmbe()) return fail(TIC_EINVAL, "rmbe handle: use tic_rmbe");
+  if (n < 0 || (n > 0 && (!d_patches || !d_idx))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  return encode_dev(h, d_patches, n, d_idx, d_preact, Prof{nullptr});
+}
+
+int tic_decode_device(tic_handle* h, const uint8_t* d_idx, int n, uint8_t* d_rgb, float* d_f32) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (h->rmbe()) return fail(TIC_EINVAL, "rmbe handle: use tic_rmbe");
+  if (n < 0 || (n > 0 && (!d_idx || (!d_rgb && !d_f32)))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  return decode_dev(h, d_idx, n, d_rgb, d_f32, Prof{nullptr});
+}
+
+int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, uint8_t* d_rgb) {
+  int rc = tic_encode_device(h, d_patches, n, d_idx, nullptr);
+  if (rc) return rc;
+  return tic_decode_device(h, d_idx, n, d_rgb, nullptr);
+}
+
+int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!h->rmbe()) return fail(TIC_EINVAL, "handle is not an rmbe handle");
+  if (n < 0 || (n > 0 && (!d_windows || !d_out))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  return rmbe_dev(h, d_windows, n, d_out, Prof{nullptr});
+}
+
+int tic_encode(tic_handle* h, const uint8_t* patches, int n, uint8_t* idx_out, float* preact_out) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (h->rmbe()) return fail(TIC_EINVAL, "rmbe handle: use tic_rmbe");
+  if (n < 0 || (n > 0 && (!patches || !idx_out))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  const size_t in_b = (size_t)n * h->P * h->P * 3, ce = (size_t)n * code_elems(h);
+  if ((rc = ensure(&h->st_in, &h->st_in_bytes, in_b))) return rc;
+  if ((rc = ensure(&h->st_out, &h->st_out_bytes, ce))) return rc;
+  if (preact_out && (rc = ensure(&h->st_out2, &h->st_out2_bytes, ce * 4))) return rc;
+  HIP_TRY(hipMemcpyAsync(h->st_in, patches, in_b, hipMemcpyHostToDevice, h->stream));
+  rc = encode_dev(h, (const uint8_t*)h->st_in, n, (uint8_t*)h->st_out, preact_out ? (float*)h->st_out2 : nullptr,
+                  Prof{nullptr});
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(idx_out, h->st_out, ce, hipMemcpyDeviceToHost, h->stream));
+  if (preact_out) HIP_TRY(hipMemcpyAsync(preact_out, h->st_out2, ce * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return TIC_OK;
+}
+
+int tic_decode(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb_out, float* f32_out) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (h->rmbe()) return fail(TIC_EINVAL, "rmbe handle: use tic_rmbe");
+  if (n < 0 || (n > 0 && (!idx || (!rgb_out && !f32_out)))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  const size_t ce = (size_t)n * code_elems(h), px = (size_t)n * h->P * h->P * 3;
+  if ((rc = ensure(&h->st_in, &h->st_in_bytes, ce))) return rc;
+  if (rgb_out && (rc = ensure(&h->st_out, &h->st_out_bytes, px))) return rc;
+  if (f32_out && (rc = ensure(&h->st_out2, &h->st_out2_bytes, px * 4))) return rc;
+  // symbols must be < Q (the LUT beyond Q is zero-filled; the reference would produce NaN/inf)
+  HIP_TRY(hipMemcpyAsync(h->st_in, idx, ce, hipMemcpyHostToDevice, h->stream));
+  rc = decode_dev(h, (const uint8_t*)h->st_in, n, rgb_out ? (uint8_t*)h->st_out : nullptr,
+                  f32_out ? (float*)h->st_out2 : nullptr, Prof{nullptr});
+  if (rc) return rc;
+  if (rgb_out) HIP_TRY(hipMemcpyAsync(rgb_out, h->st_out, px, hipMemcpyDeviceToHost, h->stream));
+  if (f32_out) HIP_TRY(hipMemcpyAsync(f32_out, h->st_out2, px * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return TIC_OK;
+}
+
+int tic_rmbe(tic_handle* h, const float* windows, int n, float* out) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!h->rmbe()) return fail(TIC_EINVAL, "handle is not an rmbe handle");
+  if (n < 0 || (n > 0 && (!windows || !out))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  const size_t b = (size_t)n * h->P * h->P * 3 * sizeof(float);
+  if ((rc = ensure(&h->st_in, &h->st_in_bytes, b))) return rc;
+  if ((rc = ensure(&h->st_out2, &h->st_out2_bytes, b))) return rc;
+  HIP_TRY(hipMemcpyAsync(h->st_in, windows, b, hipMemcpyHostToDevice, h->stream));
+  rc = rmbe_dev(h, (const float*)h->st_in, n, (float*)h->st_out2, Prof{nullptr});
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, h->st_out2, b, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return TIC_OK;
+}
+
+int tic_num_layers(const tic_handle* h) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  return (int)h->layers.size();
+}
+
+int tic_layer_info(const tic_handle* h, int i, char* name_buf, int name_len, int* kind, int* cin, int* cout,
+                   int* act, int* stage, int* residual) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (i < 0 || i >= (int)h->layers.size()) return fail(TIC_EINVAL, "layer index %d out of range", i);
+  return fill_layer_info(h->layers[i].def, name_buf, name_len, kind, cin, cout, act, stage, residual);
+}
+
+int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float* ms_out) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!d_in || n <= 0 || iters <= 0 || !ms_out) return fail(TIC_EINVAL, "bad arguments");
+  if (n > h->chunk) return fail(TIC_EINVAL, "profile n %d exceeds chunk %d", n, h->chunk);
+  const int L = (int)h->layers.size();
+  std::vector<hipEvent_t> ev(2 * L);
+  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  std::vector<double> acc(L, 0.0);
+  void *d_idx = nullptr, *d_out = nullptr;
+  const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
+  const size_t px = (size_t)n * h->P * h->P * 3;
+  HIP_TRY(hipMalloc(&d_idx, std::max<size_t>(ce, 16)));
+  HIP_TRY(hipMalloc(&d_out, px * (h->rmbe() ? 4 : 1)));
+  for (int it = 0; it < iters && rc == TIC_OK; ++it) {
+    if (h->rmbe()) {
+      rc = rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{ev.data()});
+    } else {
+      rc = encode_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, nullptr, Prof{ev.data()});
+      if (!rc) rc = decode_dev(h, (const uint8_t*)d_idx, n, (uint8_t*)d_out, nullptr, Prof{ev.data()});
+    }
+    if (rc) break;
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) rc = fail(TIC_EHIP, "profile sync: %s", hipGetErrorString(e));
+    for (int i = 0; i < L && !rc; ++i) {
+      float ms = 0.f;
+      e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
+      if (e != hipSuccess) rc = fail(TIC_EHIP, "hipEventElapsedTime: %s", hipGetErrorString(e));
+      acc[i] += ms;
+    }
+  }
+  for (int i = 0; i < L; ++i) ms_out[i] = (float)(acc[i] / iters);
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  (void)hipFree(d_idx);
+  (void)hipFree(d_out);
+  return rc;
+}
+
+int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int n, int H, int W, int cin, int cout,
+                       const float* w_host, const float* b_host, const float* d_res, float* d_out) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (kind < 0 || kind > 2 || (act != 0 && act != 1) || n <= 0 || H <= 0 || W <= 0 || !d_in || !d_out || !w_host ||
+      !b_host)
+    return fail(TIC_EINVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(h->device));
+  const tic::ConvEntry* e = find_conv(kind, cin, cout, act, d_res ? 1 : 0, tic::IN_F32, tic::OUT_F32);
+  if (!e)
+    return fail(TIC_EUNSUPPORTED, "no compiled conv3x3 for kind %d %d->%d act %d res %d", kind, cin, cout, act,
+                d_res ? 1 : 0);
+  std::vector<float> wp;
+  pack_generic(w_host, kind, cin, cout, &wp);
+  float *d_w = nullptr, *d_b = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_w, wp.size() * 4));
+  HIP_TRY(hipMalloc((void**)&d_b, (size_t)cout * 4));
+  HIP_TRY(hipMemcpy(d_w, wp.data(), wp.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d_b, b_host, (size_t)cout * 4, hipMemcpyHostToDevice));
+  tic::ConvArgs a{};
+  a.in = d_in;
+  a.wp = d_w;
+  a.bias = d_b;
+  a.res = d_res;
+  a.out = d_out;
+  a.H = H;
+  a.W = W;
+  a.Ho = out_size(kind, H);
+  a.Wo = out_size(kind, W);
+  a.pad_y = same_pad(kind, H);
+  a.pad_x = same_pad(kind, W);
+  e->fn(a, n, h->stream);
+  int rc = check_launch();
+  hipError_t se = hipStreamSynchronize(h->stream);
+  (void)hipFree(d_w);
+  (void)hipFree(d_b);
+  if (rc) return rc;
+  if (se != hipSuccess) return fail(TIC_EHIP, "conv3x3 sync: %s", hipGetErrorString(se));
+  return TIC_OK;
+}
+
+int tic_device_info(tic_handle* h, char* buf, int len) {
+  if (!h || !buf || len <= 0) return fail(TIC_EINVAL, "bad arguments");
+  hipDeviceProp_t p;
+  HIP_TRY(hipGetDeviceProperties(&p, h->device));
+  snprintf(buf, len, "%s | %s | CUs %d | HBM %.1f GB | device %d", p.name, p.gcnArchName, p.multiProcessorCount,
+           p.totalGlobalMem / 1e9, h->device);
+  return TIC_OK;
+}
+
+}  // extern "C"
