@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark: encode+decode MPix/s on 256x256 RGB patches (BASELINE.json metric).
+
+A step = one encode->decode pass (uint8 patches -> symbols -> uint8 reconstruction) of
+one batch of synthetic patches already resident in HBM.  Default workload =
+BASELINE.json configs[1]: model_0, batch 64, 256x256.  Multi-GPU: one process per GPU
+(launched by torch.distributed.run), images sharded, weak scaling, no data-path
+collective; RCCL is used for the barrier / max-over-ranks timing and the final
+all-gather of per-rank stats.  Rank 0 prints ONE JSON line.
+
+No PyTorch is imported in this process (torch bundles a second HIP runtime); the
+torch.distributed launcher only provides RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA / vector peak (spec)
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--patch", type=int, default=256)
+    ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
+    return ap.parse_args()
+
+
+def kernel_groups(codec, model_id, P, ms):
+    """Group layers by the kernel instance they launch (same template args + shape)."""
+    from tf_image_compression_amd.topology import layer_work, RMBE_ID, weight_bytes
+    work = layer_work(model_id, P)
+    L = len(work)
+    n_enc = sum(1 for lay, *_ in work if lay.stage == "enc")
+    groups = {}
+    rows = []
+    for i, (lay, flops, nbytes, ho) in enumerate(work):
+        role = "rgb_in" if i == 0 else ("rgb_out" if i == L - 1 else
+                                        ("quant" if (model_id != RMBE_ID and i == n_enc - 1) else
+                                         ("dequant" if (model_id != RMBE_ID and i == n_enc) else "f32")))
+        key = (lay.kind, lay.cin, lay.cout, lay.act, lay.residual, role, ho)
+        rows.append({"layer": lay.name, "kind": lay.kind, "cin": lay.cin, "cout": lay.cout, "out_hw": ho,
+                     "ms": float(ms[i]), "flops_per_patch": flops, "bytes_per_patch": nbytes,
+                     "weight_bytes": weight_bytes(lay), "key": list(map(str, key))})
+        g = groups.setdefault(key, {"layers": [], "ms": 0.0, "flops": flops, "bytes": nbytes,
+                                    "wbytes": weight_bytes(lay)})
+        g["layers"].append(lay.name)
+        g["ms"] += float(ms[i])
+    return groups, rows
+
+
+def roofline_of(group, batch):
+    flops = group["flops"] * batch
+    nbytes = group["bytes"] * batch + group["wbytes"]
+    ms = group["ms"] / len(group["layers"])  # mean duration per launch
+    t_c = flops / (PEAK_FP32_TFLOPS * 1e12)
+    t_m = nbytes / (PEAK_HBM_GBS * 1e9)
+    if t_m > t_c:
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4)}, ms, flops, nbytes
+    achieved = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4)}, ms, flops, nbytes
+
+
+def step_roofline(rows, batch, step_ms):
+    t_min = 0.0
+    for r in rows:
+        f = r["flops_per_patch"] * batch
+        b = r["bytes_per_patch"] * batch + r["weight_bytes"]
+        t_min += max(f / (PEAK_FP32_TFLOPS * 1e12), b / (PEAK_HBM_GBS * 1e9))
+    return t_min * 1e3 / step_ms
+
+
+def cpu_baseline(model_id, P, params, mean, std, target_s):
+    """The oracle (numpy, float32 GEMMs on OpenBLAS) timed on this box's host cores on a
+    bounded sample of the same workload; the reference's TF-CPU path cannot run here."""
+    from oracle import tic_oracle as o
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    cores = min(16, os.cpu_count() or 1)
+    n = 8
+    x = np.random.default_rng(99).integers(0, 256, (n, P, P, 3), dtype=np.uint8)
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    times = []
+    try:
+        t_begin = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            _, idx = o.encoder(params, mean, std, x, P, 2, model_id, acc=np.float32)
+            o.decoder(params, mean, std, idx, 2, model_id, acc=np.float32)
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_begin > target_s and len(times) >= 3:
+                break
+    finally:
+        if ctx is not None:
+            ctx.unregister() if hasattr(ctx, "unregister") else None
+    med = float(np.median(times))
+    return {"value": round(n * P * P / med / 1e6, 3), "unit": "MPix/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/tic_oracle.py float32 (OpenBLAS {cores} threads), model_{model_id} "
+                      f"{n} x {P}x{P} patches encode+decode, median of {len(times)} runs "
+                      f"({sum(times):.1f} s total)"}
+
+
+def parity_probe(codec, model_id, P, params, mean, std):
+    """Delta-PSNR vs the oracle on 2 structured patches (rank 0, outside the timed region)."""
+    from oracle import tic_oracle as o
+    r = np.random.default_rng(5)
+    yy, xx = np.meshgrid(np.arange(P), np.arange(P), indexing="ij")
+    pats = np.stack([np.clip(128 + 50 * np.sin(0.05 * (k + 1) * xx) * np.cos(0.03 * yy)[..., None].repeat(1, -1)
+                             + r.normal(0, 8, (P, P, 3)), 0, 255).astype(np.uint8) for k in range(2)])
+    idx, pre = codec.encode(pats, return_preact=True)
+    ref_pre, ref_idx = o.encoder(params, mean, std, pats, P, 2, model_id)
+    scale = max(1.0, float(np.abs(ref_pre).max()))
+    safe = o.decision_margin(ref_pre, 2) > 1e-5 * scale
+    rgb = codec.decode(idx)
+    _, ref_u8 = o.decoder(params, mean, std, idx, 2, model_id)
+    p_gpu = o.dataset_psnr(list(zip(pats, rgb)))
+    p_ref = o.dataset_psnr(list(zip(pats, ref_u8)))
+    return {"delta_psnr_db": round(abs(p_gpu - p_ref), 5),
+            "symbol_mismatch_outside_band": int(np.count_nonzero((idx != ref_idx) & safe)),
+            "symbols": int(idx.size)}
+
+
+def main():
+    args = parse()
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import bottleneck_shape
+    from tf_image_compression_amd import dist
+
+    rank, world, local = dist.env_rank()
+    if world != args.gpus:
+        # single-process run with --gpus 1, or a launcher mismatch
+        if not (world == 1 and args.gpus == 1):
+            print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    P, B, M = args.patch, args.batch, args.model
+    params = synthetic_params(M, seed=0)
+    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local)
+    comm = dist.make_comm(codec)
+    eh, ew, ec = bottleneck_shape(M, P)
+
+    x = np.random.default_rng(1234 + rank).integers(0, 256, (B, P, P, 3), dtype=np.uint8)
+    d_in = codec.alloc(x.nbytes)
+    d_in.upload(x)
+    d_idx = codec.alloc(B * eh * ew * ec)
+    d_rgb = codec.alloc(x.nbytes)
+
+    for _ in range(args.warmup):
+        codec.codec_device(d_in, B, d_idx, d_rgb)
+    codec.synchronize()
+    comm.barrier()
+    codec.synchronize()
+    t0 = time.perf_counter()
+    wall0 = time.time()
+    for _ in range(args.steps):
+        codec.codec_device(d_in, B, d_idx, d_rgb)
+    codec.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    wall1 = time.time()
+    t_max = comm.allreduce_max(elapsed)
+
+    # per-rank stats -> the one RCCL all-gather (SSE of the last reconstruction)
+    rec = d_rgb.download(x.shape, np.uint8)
+    sse = float(np.sum(np.square(rec.astype(np.float64) - x.astype(np.float64))))
+    st = dist.RankStats(sse=sse * args.steps, dims=x.size * args.steps, bits=B * eh * ew * ec * args.steps,
+                        images=B * args.steps, t_start=wall0, t_end=wall1)
+    gathered = comm.allgather_stats(st)
+    summary = dist.combine(gathered)
+
+    # per-layer kernel timing (HIP events on the codec's stream), outside the timed region
+    ms = codec.profile_layers(d_in, B, args.profile_iters)
+    groups, rows = kernel_groups(codec, M, P, ms)
+    dom_key = max(groups, key=lambda k: groups[k]["ms"])
+    roof, dom_ms, dom_flops, dom_bytes = roofline_of(groups[dom_key], B)
+    roof["traffic"] = None
+    traffic_file = os.path.join(ROOT, "profiles", "traffic_r01.json")
+    if os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file))
+            ent = tr.get(",".join(map(str, dom_key)))
+            if ent is not None:
+                roof["traffic"] = ent
+        except Exception:
+            pass
+    roof["kernel"] = "+".join(groups[dom_key]["layers"])
+    roof["ms_per_launch"] = round(dom_ms, 5)
+
+    step_ms = t_max * 1e3 / args.steps
+    total_px = world * B * P * P * args.steps
+    value = total_px / t_max / 1e6
+    out = {
+        "metric": "encode+decode MPix/s at 256x256 RGB",
+        "value": round(value, 2),
+        "unit": "MPix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic uniform u8 patches (seed 1234+rank), seeded He-normal weights",
+        "config": {"workload": f"model_{M} encode+decode, batch={B} patches of {P}x{P} RGB per GPU",
+                   "model": f"model_{M}", "global_batch": B * world, "patch": P,
+                   "code_shape": [eh, ew, ec], "parallelism": f"image-parallel x{world}"},
+        "roofline": roof,
+        "roofline_step_frac": round(step_roofline(rows, B, step_ms), 4),
+        "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
+                            "raw_bpp": round(summary["bpp"], 4)},
+    }
+    if rank == 0:
+        try:
+            os.makedirs(os.path.dirname(args.layers_out), exist_ok=True)
+            json.dump({"config": out["config"], "step_ms": step_ms, "layers": rows,
+                       "groups": {",".join(map(str, k)): {"layers": g["layers"], "ms": g["ms"]}
+                                  for k, g in groups.items()}},
+                      open(args.layers_out, "w"), indent=1)
+        except OSError:
+            pass
+        out["parity"] = parity_probe(codec, M, P, params, SYNTH_MEAN, SYNTH_STD)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(M, P, params, SYNTH_MEAN, SYNTH_STD, args.cpu_seconds)
+            out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    comm.close()
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()

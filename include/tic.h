@@ -119,6 +119,10 @@ int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float*
 int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int n, int H, int W, int cin,
                        int cout, const float* w_host, const float* b_host, const float* d_res, float* d_out);
 
+/* The handle's HIP stream (hipStream_t as void*), e.g. to enqueue an RCCL collective
+ * behind the codec's kernels. */
+int tic_get_stream(tic_handle* h, void** stream);
+
 /* Device info string (name, CUs, arch) for logs. */
 int tic_device_info(tic_handle* h, char* buf, int len);
 

@@ -50,6 +50,7 @@ SIGNATURES = [
     ("tic_profile_layers", C.c_int, [vp, vp, C.c_int, C.c_int, f32p]),
     ("tic_conv3x3_device", C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      f32p, f32p, vp, vp]),
+    ("tic_get_stream", C.c_int, [vp, C.POINTER(vp)]),
     ("tic_device_info", C.c_int, [vp, C.c_char_p, C.c_int]),
 ]
 

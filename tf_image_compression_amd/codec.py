@@ -164,6 +164,11 @@ class Codec:
     def rmbe_device(self, d_in: DeviceBuffer, n: int, d_out: DeviceBuffer):
         check(lib().tic_rmbe_device(self._h, d_in.ptr, n, d_out.ptr), "tic_rmbe_device")
 
+    def stream_ptr(self) -> C.c_void_p:
+        s = C.c_void_p()
+        check(lib().tic_get_stream(self._h, C.byref(s)), "tic_get_stream")
+        return s
+
     def synchronize(self) -> None:
         check(lib().tic_synchronize(self._h), "tic_synchronize")
 

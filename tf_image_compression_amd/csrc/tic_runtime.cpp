@@ -803,6 +803,12 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   return TIC_OK;
 }
 
+int tic_get_stream(tic_handle* h, void** stream) {
+  if (!h || !stream) return fail(TIC_EINVAL, "null argument");
+  *stream = (void*)h->stream;
+  return TIC_OK;
+}
+
 int tic_device_info(tic_handle* h, char* buf, int len) {
   if (!h || !buf || len <= 0) return fail(TIC_EINVAL, "bad arguments");
   hipDeviceProp_t p;

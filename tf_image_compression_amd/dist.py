@@ -1,0 +1,244 @@
+"""Image-parallel sharding and the one collective of the codec: an all-gather of
+per-rank rate / distortion statistics.
+
+One process per GPU (``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``MASTER_ADDR``/
+``MASTER_PORT`` from the launcher's environment).  Images are independent, so the
+data path has no collective at all; at the end each rank contributes a 48-byte
+``RankStats`` record and every rank computes the dataset PSNR exactly as
+processing_utils/evaluate.py:10-32 does (sum of SSE over sum of dims), the bpp as
+bytes*8/pixels (evaluate.py:45-50) and the throughput as total pixels over
+(max end - min start).
+
+Backends:
+* ``RcclComm`` — RCCL (librccl.so, ctypes) over xGMI on the codec's HIP stream; the
+  ncclUniqueId is bootstrapped through a tiny TCP exchange on MASTER_ADDR.  Used by
+  bench.py / the CLIs on GPU boxes.  No PyTorch is imported in GPU processes (torch
+  bundles a second HIP runtime with the same soname).
+* ``GlooComm`` — torch.distributed gloo on CPU, for the world_size-2 CPU tests of the
+  same orchestration code.
+* ``LocalComm`` — world size 1.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import socket
+import struct
+import time
+from dataclasses import dataclass
+
+import numpy as np
+
+STATS_FIELDS = ("sse", "dims", "bits", "images", "t_start", "t_end")
+
+
+@dataclass
+class RankStats:
+    sse: float = 0.0      # sum of squared errors over the rank's images (float64)
+    dims: int = 0         # number of sample values (H*W*3 per image)
+    bits: int = 0         # raw code bits (or coded bytes*8 once entropy coded)
+    images: int = 0
+    t_start: float = 0.0  # wall clock (time.time()) at the start of the rank's work
+    t_end: float = 0.0
+
+    def to_array(self) -> np.ndarray:
+        return np.array([self.sse, self.dims, self.bits, self.images, self.t_start, self.t_end], np.float64)
+
+    @staticmethod
+    def from_array(a) -> "RankStats":
+        a = np.asarray(a, np.float64)
+        return RankStats(float(a[0]), int(a[1]), int(a[2]), int(a[3]), float(a[4]), float(a[5]))
+
+
+def combine(stats: list[RankStats]) -> dict:
+    """Global metrics from every rank's record (processing_utils/evaluate.py:10-32,45-50)."""
+    sse = sum(s.sse for s in stats)
+    dims = sum(s.dims for s in stats)
+    bits = sum(s.bits for s in stats)
+    pixels = dims / 3.0
+    t0 = min(s.t_start for s in stats)
+    t1 = max(s.t_end for s in stats)
+    psnr = float("inf") if sse == 0 else 20.0 * np.log10(255.0) - 10.0 * np.log10(sse / max(dims, 1))
+    return {
+        "psnr_db": float(psnr),
+        "bpp": bits / pixels if pixels else 0.0,
+        "images": sum(s.images for s in stats),
+        "pixels": int(pixels),
+        "seconds": t1 - t0,
+        "mpix_per_s": pixels / (t1 - t0) / 1e6 if t1 > t0 else float("nan"),
+    }
+
+
+def shard_range(n_items: int, rank: int, world: int) -> tuple[int, int]:
+    """Static contiguous split [r*ceil(M/W), ...): rank r gets items [lo, hi)."""
+    per = -(-n_items // world)
+    lo = min(n_items, rank * per)
+    return lo, min(n_items, lo + per)
+
+
+def env_rank() -> tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+class LocalComm:
+    rank, world = 0, 1
+
+    def barrier(self):
+        pass
+
+    def allreduce_max(self, x: float) -> float:
+        return float(x)
+
+    def allgather_stats(self, s: RankStats) -> list[RankStats]:
+        return [s]
+
+    def close(self):
+        pass
+
+
+class GlooComm:
+    """torch.distributed (gloo, CPU) — for CPU tests of the multi-rank path only."""
+
+    def __init__(self):
+        import torch.distributed as dist  # imported lazily: never in GPU processes
+        self.dist = dist
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def allreduce_max(self, x: float) -> float:
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allgather_stats(self, s: RankStats) -> list[RankStats]:
+        import torch
+        t = torch.from_numpy(s.to_array())
+        out = [torch.zeros(6, dtype=torch.float64) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [RankStats.from_array(o.numpy()) for o in out]
+
+    def close(self):
+        self.dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------- RCCL
+NCCL_FLOAT64 = 8
+NCCL_MAX = 2
+NCCL_UNIQUE_ID_BYTES = 128
+
+
+class _NcclUniqueId(C.Structure):
+    _fields_ = [("internal", C.c_char * NCCL_UNIQUE_ID_BYTES)]
+
+
+def _recv_exact(sock, n):
+    buf = b""
+    while len(buf) < n:
+        chunk = sock.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("rendezvous peer closed")
+        buf += chunk
+    return buf
+
+
+def exchange_unique_id(rank: int, world: int, payload: bytes | None, addr: str, port: int,
+                       timeout: float = 120.0) -> bytes:
+    """Rank 0 serves `payload` (the 128-byte ncclUniqueId) to world-1 peers over TCP."""
+    if world == 1:
+        return payload
+    if rank == 0:
+        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        srv.bind((addr, port))
+        srv.listen(world)
+        srv.settimeout(timeout)
+        try:
+            for _ in range(world - 1):
+                conn, _ = srv.accept()
+                with conn:
+                    conn.sendall(struct.pack("!I", len(payload)) + payload)
+        finally:
+            srv.close()
+        return payload
+    deadline = time.time() + timeout
+    while True:
+        try:
+            with socket.create_connection((addr, port), timeout=5.0) as s:
+                (ln,) = struct.unpack("!I", _recv_exact(s, 4))
+                return _recv_exact(s, ln)
+        except (ConnectionRefusedError, socket.timeout, OSError):
+            if time.time() > deadline:
+                raise
+            time.sleep(0.05)
+
+
+class RcclComm:
+    """RCCL communicator over the codec's HIP stream (ctypes; no PyTorch)."""
+
+    def __init__(self, codec, rank: int, world: int, addr: str | None = None, port: int | None = None):
+        self.rank, self.world, self.codec = rank, world, codec
+        self.nccl = C.CDLL(os.environ.get("TIC_RCCL", "/opt/rocm/lib/librccl.so.1"))
+        self.nccl.ncclGetUniqueId.argtypes = [C.POINTER(_NcclUniqueId)]
+        self.nccl.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int, _NcclUniqueId, C.c_int]
+        self.nccl.ncclAllGather.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p]
+        self.nccl.ncclAllReduce.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p]
+        self.nccl.ncclGetErrorString.restype = C.c_char_p
+        self.nccl.ncclCommDestroy.argtypes = [C.c_void_p]
+        uid = _NcclUniqueId()
+        if rank == 0:
+            self._ok(self.nccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
+        addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = port or int(os.environ.get("TIC_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 17))
+        raw = exchange_unique_id(rank, world, bytes(uid.internal) if rank == 0 else None, addr, port)
+        C.memmove(C.addressof(uid), raw, NCCL_UNIQUE_ID_BYTES)
+        self.comm = C.c_void_p()
+        self._ok(self.nccl.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
+        self.stream = codec.stream_ptr()
+        self.d_send = codec.alloc(8 * 6)
+        self.d_recv = codec.alloc(8 * 6 * world)
+
+    def _ok(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.nccl.ncclGetErrorString(rc).decode()} ({rc})")
+
+    def allreduce_max(self, x: float) -> float:
+        self.d_send.upload(np.array([x], np.float64))
+        self._ok(self.nccl.ncclAllReduce(self.d_send.ptr, self.d_recv.ptr, 1, NCCL_FLOAT64, NCCL_MAX, self.comm,
+                                         self.stream), "ncclAllReduce")
+        self.codec.synchronize()
+        return float(self.d_recv.download((1,), np.float64)[0])
+
+    def barrier(self):
+        self.allreduce_max(0.0)
+
+    def allgather_stats(self, s: RankStats) -> list[RankStats]:
+        self.d_send.upload(s.to_array())
+        self._ok(self.nccl.ncclAllGather(self.d_send.ptr, self.d_recv.ptr, 6, NCCL_FLOAT64, self.comm, self.stream),
+                 "ncclAllGather")
+        self.codec.synchronize()
+        a = self.d_recv.download((self.world, 6), np.float64)
+        return [RankStats.from_array(r) for r in a]
+
+    def close(self):
+        if self.comm:
+            self.nccl.ncclCommDestroy(self.comm)
+            self.comm = None
+
+
+def make_comm(codec=None):
+    """LocalComm at world size 1, RcclComm on a GPU codec otherwise."""
+    rank, world, _ = env_rank()
+    if world == 1:
+        return LocalComm()
+    if codec is None:
+        return GlooComm()
+    return RcclComm(codec, rank, world)
