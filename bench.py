@@ -125,10 +125,8 @@ def cpu_baseline(model_id, P, params, mean, std, target_s):
 def parity_probe(codec, model_id, P, params, mean, std):
     """Delta-PSNR vs the oracle on 2 structured patches (rank 0, outside the timed region)."""
     from oracle import tic_oracle as o
-    r = np.random.default_rng(5)
-    yy, xx = np.meshgrid(np.arange(P), np.arange(P), indexing="ij")
-    pats = np.stack([np.clip(128 + 50 * np.sin(0.05 * (k + 1) * xx) * np.cos(0.03 * yy)[..., None].repeat(1, -1)
-                             + r.normal(0, 8, (P, P, 3)), 0, 255).astype(np.uint8) for k in range(2)])
+    from tf_image_compression_amd.synthetic import structured_patches
+    pats = structured_patches(2, P, seed=5)
     idx, pre = codec.encode(pats, return_preact=True)
     ref_pre, ref_idx = o.encoder(params, mean, std, pats, P, 2, model_id)
     scale = max(1.0, float(np.abs(ref_pre).max()))

@@ -1,0 +1,143 @@
+"""CPU tests of the C-ABI boundary: libtic.so loads, exports exactly what include/tic.h
+declares, its layer tables agree with the host mirror and with the oracle's independent
+tables, and argument validation fails loudly without touching a device."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import tic_oracle as o
+
+HEADER = os.path.join(ROOT, "include", "tic.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(tic_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from tf_image_compression_amd import _lib
+    return _lib.lib()
+
+
+def test_library_exports_every_header_symbol(L):
+    names = header_functions()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in include/tic.h but not exported"
+
+
+def test_binding_covers_header():
+    from tf_image_compression_amd import _lib
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert bound == set(header_functions())
+
+
+def test_exports_are_c_symbols():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "tf_image_compression_amd", "libtic.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for n in header_functions():
+        assert n in exported  # unmangled: extern "C"
+
+
+def _native_table(L, model_id):
+    out = []
+    for i in range(L.tic_model_num_layers(model_id)):
+        name = C.create_string_buffer(128)
+        v = [C.c_int() for _ in range(6)]
+        assert L.tic_model_layer(model_id, i, name, 128, *[C.byref(x) for x in v]) == 0
+        out.append((name.value.decode(), *[x.value for x in v]))
+    return out
+
+
+@pytest.mark.parametrize("model_id", [0, 1, 2, 3, 100])
+def test_native_table_matches_host_and_oracle(L, model_id):
+    from tf_image_compression_amd.topology import layer_table
+    kinds = {"conv_s1": 0, "conv_s2": 1, "convT": 2}
+    host = [(l.name, kinds[l.kind], l.cin, l.cout, 1 if l.act == "relu" else 0, 0 if l.stage == "enc" else 1,
+             int(l.residual)) for l in layer_table(model_id)]
+    assert _native_table(L, model_id) == host
+    # the oracle's independently written tables: same TF variable names and shapes
+    if model_id == 100:
+        shapes = o.param_shapes(o.RMBE)
+    else:
+        shapes = o.param_shapes(o.MODELS[model_id][0] + o.MODELS[model_id][1])
+    from tf_image_compression_amd.topology import param_shapes
+    assert param_shapes(model_id) == shapes
+
+
+def test_argument_errors_without_device(L):
+    h = C.c_void_p()
+    assert L.tic_create(7, 256, 2, 0, C.byref(h)) == -1
+    assert b"unknown model" in L.tic_last_error()
+    assert L.tic_create(0, 255, 2, 0, C.byref(h)) == -1
+    assert L.tic_create(0, 256, 1, 0, C.byref(h)) == -1
+    assert L.tic_create(0, 256, 300, 0, C.byref(h)) == -1
+    assert L.tic_create(0, 200, 2, 0, C.byref(h)) == -1
+    assert b"divisible" in L.tic_last_error()
+    assert L.tic_model_num_layers(99) == -1
+    assert L.tic_encode(None, None, 1, None, None) == -1
+    assert L.tic_decode(None, None, 1, None, None) == -1
+    assert L.tic_set_param(None, b"x", None, None, 0) == -1
+    assert L.tic_finalize(None) == -1
+    assert L.tic_synchronize(None) == -1
+
+
+def test_python_wrapper_raises_not_falls_back(monkeypatch):
+    """No CPU fallback: a missing library is a hard error."""
+    from tf_image_compression_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libtic.so")
+    with pytest.raises(_lib.TicError):
+        _lib.lib()
+
+
+def test_product_package_never_imports_oracle():
+    """The oracle is test infrastructure: no product module may reference it."""
+    pkg = os.path.join(ROOT, "tf_image_compression_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f
+    for f in ("encode.py", "decode.py"):
+        p = os.path.join(ROOT, f)
+        if os.path.exists(p):
+            assert not re.search(r"^\s*(from|import)\s+oracle", open(p).read(), re.M)
+
+
+def test_weights_and_topology_host_side():
+    from tf_image_compression_amd.weights import synthetic_params, check_params, save_params, load_params
+    from tf_image_compression_amd.topology import bottleneck_shape, layer_work
+    p = synthetic_params(0)
+    check_params(0, p)
+    bad = dict(p)
+    bad["encode_0/kernel"] = bad["encode_0/kernel"][..., :5]
+    with pytest.raises(ValueError):
+        check_params(0, bad)
+    del bad["encode_0/kernel"]
+    with pytest.raises(ValueError):
+        check_params(0, bad)
+    assert bottleneck_shape(0, 256) == (16, 16, 64)
+    assert bottleneck_shape(3, 256) == (16, 16, 80)
+    assert bottleneck_shape(3, 128) == (8, 8, 80)
+    assert bottleneck_shape(2, 128) == (8, 8, 64)
+    flops = sum(r[1] for r in layer_work(0, 256))
+    assert abs(flops - 509.607936e6) < 1
+    assert abs(sum(r[1] for r in layer_work(3, 256)) - 3878.682624e6) < 1
+
+
+def test_npz_round_trip(tmp_path):
+    from tf_image_compression_amd.weights import synthetic_params, save_params, load_params
+    p = synthetic_params(2)
+    save_params(str(tmp_path / "w.npz"), p)
+    q = load_params(str(tmp_path / "w"))
+    assert set(p) == set(q) and all(np.array_equal(p[k], q[k]) for k in p)

@@ -440,6 +440,14 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (patch_size < 16 || patch_size % 2 != 0 || patch_size > 8192)
     return fail(TIC_EINVAL, "patch_size %d must be even and in [16, 8192]", patch_size);
   if (quan_scale < 2 || quan_scale > 256) return fail(TIC_EINVAL, "quan_scale %d must be in [2, 256]", quan_scale);
+  {  // geometry: the decoder must return to patch_size (P divisible by 2^#stride-2 layers)
+    int g = patch_size;
+    for (const LayerDef& d : table) g = out_size(d.kind, g);
+    if (g != patch_size)
+      return fail(TIC_EINVAL, "patch_size %d: decoder output would be %dx%d (patch_size must be divisible by 2^%d)",
+                  patch_size, g, g,
+                  (int)std::count_if(table.begin(), table.end(), [](const LayerDef& d) { return d.kind == K_S2; }));
+  }
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(TIC_EINVAL, "device %d not available (%d visible)", device, ndev);
@@ -462,11 +470,6 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
     h->layers.push_back(std::move(l));
   }
   h->act_elems = act;
-  if (!table.empty() && hh != patch_size) {
-    delete h;
-    return fail(TIC_EINVAL, "patch_size %d: decoder output would be %dx%d (needs %d stride-2 halvings to stay even)",
-                patch_size, hh, hh, (int)std::count_if(table.begin(), table.end(), [](const LayerDef& d) { return d.kind == K_S2; }));
-  }
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
