@@ -112,6 +112,14 @@ int tic_model_layer(int model_id, int i, char* name_buf, int name_len, int* kind
  * ms_out[i] (size >= tic_num_layers). */
 int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float* ms_out);
 
+/* Measure every compiled tiling of every layer on the live buffers of one encode+decode
+ * (or rmbe) pass over d_in[n] and keep the fastest per layer for batch size n (like
+ * cuDNN's benchmark mode).  Untuned batch sizes use a grid-size heuristic. */
+int tic_autotune(tic_handle* h, const void* d_in, int n, int reps);
+/* Tiling used by layer i for batch n: rows per workgroup and channel split, the latter
+ * + 100 when the weights are staged through LDS (0,0 if the layer has one fixed kernel). */
+int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit);
+
 /* Unit-test entry: one layer on device float32 NHWC tensors.
  * kind/act as tic_layer_info; res (nullable) is added after the activation.
  * w is the TF-layout kernel (HWIO for conv, [3,3,Cout,Cin] for conv-T), host memory.

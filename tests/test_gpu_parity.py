@@ -37,6 +37,8 @@ def lib_codec():
         c.close()
 
 
+TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1)] for wl in (0, 1)]
+
 LAYER_CASES = [
     (K_S1, 64, 64, 1, False, 16, 16),
     (K_S1, 64, 64, 1, True, 20, 13),
@@ -78,14 +80,30 @@ def test_conv3x3_layer(lib_codec, kind, cin, cout, act, res, H, W):
     if res:
         d_res = codec.alloc(resid.nbytes)
         d_res.upload(resid)
-    codec.conv3x3_device(kind, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
-    got = d_out.download(ref.shape, np.float32)
+    import os
+    from tf_image_compression_amd._lib import TicError
+    outs = []
+    try:
+        for th, ns, wl in TILES:
+            os.environ["TIC_FORCE_TILE"] = f"{th},{ns},{wl}"
+            try:
+                codec.conv3x3_device(kind, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
+            except TicError as e:
+                assert "no compiled" in str(e)
+                continue
+            outs.append(((th, ns, wl), d_out.download(ref.shape, np.float32)))
+    finally:
+        os.environ.pop("TIC_FORCE_TILE", None)
     for buf in (d_in, d_out, d_res):
         if buf is not None:
             buf.free()
+    assert outs, "no compiled tiling for this layer"
     scale = max(1.0, float(np.max(np.abs(ref))))
-    err = float(np.max(np.abs(got - ref)))
-    assert err <= 3e-5 * scale, (err, scale)
+    for tile, got in outs:
+        err = float(np.max(np.abs(got - ref)))
+        assert err <= 3e-5 * scale, (tile, err, scale)
+        # every tiling runs the same per-output fma order: results are bit-identical
+        assert np.array_equal(got, outs[0][1]), tile
 
 
 def _check_codec(codec, params, model_id, P, patches, Q=2):
@@ -149,6 +167,29 @@ def test_codec_model0_full_size(lib_codec):
     assert np.array_equal(rgb64[:4], rgb4)
     # determinism
     assert np.array_equal(codec.encode(big), idx64)
+
+
+def test_autotuned_equals_default(lib_codec):
+    """Autotuning only changes tilings, never results (bit-exact)."""
+    P, n = 256, 16
+    codec, params = lib_codec(0, P)
+    x = structured_patches(n, P, seed=31)
+    ref_idx, ref_pre = codec.encode(x, return_preact=True)
+    ref_rgb = codec.decode(ref_idx)
+    d_in = codec.alloc(x.nbytes)
+    d_in.upload(x)
+    codec.autotune(d_in, n, reps=2)
+    d_idx = codec.alloc(ref_idx.nbytes)
+    d_pre = codec.alloc(ref_pre.nbytes)
+    d_rgb = codec.alloc(x.nbytes)
+    codec.encode_device(d_in, n, d_idx, d_pre)
+    codec.decode_device(d_idx, n, d_rgb)
+    codec.synchronize()
+    assert np.array_equal(d_idx.download(ref_idx.shape, np.uint8), ref_idx)
+    assert np.array_equal(d_pre.download(ref_pre.shape, np.float32), ref_pre)
+    assert np.array_equal(d_rgb.download(x.shape, np.uint8), ref_rgb)
+    for b in (d_in, d_idx, d_pre, d_rgb):
+        b.free()
 
 
 def test_quan_scale_256(lib_codec):

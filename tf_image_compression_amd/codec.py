@@ -178,6 +178,17 @@ class Codec:
         check(lib().tic_profile_layers(self._h, d_in.ptr, n, iters, ptr(ms, C.c_float)), "tic_profile_layers")
         return ms
 
+    def autotune(self, d_in: DeviceBuffer, n: int, reps: int = 5) -> None:
+        check(lib().tic_autotune(self._h, d_in.ptr, n, reps), "tic_autotune")
+
+    def layer_variants(self, n: int):
+        out = []
+        for i in range(len(self.layers())):
+            th, ns = C.c_int(), C.c_int()
+            check(lib().tic_layer_variant(self._h, i, n, C.byref(th), C.byref(ns)), "tic_layer_variant")
+            out.append((th.value, ns.value))
+        return out
+
     def conv3x3_device(self, kind: int, act: int, d_in: DeviceBuffer, n: int, H: int, W: int, cin: int,
                        cout: int, kernel: np.ndarray, bias: np.ndarray, d_res: DeviceBuffer | None,
                        d_out: DeviceBuffer) -> None:

@@ -52,16 +52,30 @@ struct TileGeom {
   static constexpr int LC = MODE == MODE_S1 ? 18 : (MODE == MODE_S2 ? 34 : 17);
 };
 
-// Grid: x = ceil(Wg/16), y = ceil(Hg/TH), z = batch, where (Hg,Wg) is the output grid
-// (S1/S2) or the input grid (T2).  256 threads = 4 waves = WR row-groups x (4/WR)
-// channel-groups; each wave owns MB = TH/WR rows of 16 pixels x NB = Cout/16/(4/WR)
-// channel blocks (x 4 phases for T2).
-template <int MODE, int CIN, int COUT, int TH, int WR, int ACT, bool RES, int IN, int OUT>
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Grid: x = ceil(Wg/16) * NSPLIT, y = ceil(Hg/TH), z = batch, where (Hg,Wg) is the
+// output grid (S1/S2) or the input grid (T2).  NSPLIT workgroups share a pixel tile and
+// split the output channels.  256 threads = 4 waves = WR row-groups x (4/WR) channel
+// groups; each wave owns MB = TH/WR rows of 16 pixels x NB channel blocks of 16
+// (x 4 phases for T2).
+//
+// The K loop is a flat, fully unrolled list of steps, tap-major for every mode (step =
+// one 16-channel chunk of one 3x3 tap), so every tiling accumulates each output in the
+// same fma order (results are bit-identical across tilings).  Weights are packed
+// [tap][Cin/16][4 g][Cout][4 t]; their A fragments come either
+//   WLDS=false: straight from L2 into registers, prefetched PF steps ahead, or
+//   WLDS=true : from a 2-slot LDS ring holding one tap's slab for this workgroup's
+//               channels, filled by LDS-DMA (global_load_lds_dwordx4) one tap ahead and
+//               shared by the 4 waves (one barrier per tap).
+template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, bool WLDS, int ACT, bool RES, int IN, int OUT>
 __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
   static_assert(CIN % 16 == 0 && COUT % 16 == 0, "channels must be multiples of 16");
   constexpr int PS = CIN + 8;
   constexpr int KC = CIN / 16;
-  constexpr int NBT = COUT / 16;
+  constexpr int COUT_WG = COUT / NSPLIT;
+  static_assert(COUT_WG % 16 == 0, "bad channel split");
+  constexpr int NBT = COUT_WG / 16;
   constexpr int WC = 4 / WR;
   static_assert(WR * WC == 4 && TH % WR == 0 && NBT % WC == 0, "bad wave split");
   constexpr int NB = NBT / WC;
@@ -70,50 +84,21 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
   constexpr int LR = TileGeom<MODE, TH>::LR;
   constexpr int LC = TileGeom<MODE, TH>::LC;
   constexpr int C4 = CIN / 4;
+  constexpr int NSTEP = 9 * KC;
+  constexpr int TILE = LR * LC * PS;            // floats of the input tile
+  constexpr int WSLAB = CIN * COUT_WG;          // floats of one tap's weights for this WG
+  constexpr int WCHUNK = WSLAB / 4;             // 16-byte chunks per slab (multiple of 64)
 
-  __shared__ __attribute__((aligned(16))) float lds[LR * LC * PS];
+  // ONE __shared__ array (a second object can make hipcc drain the LDS-DMA early)
+  __shared__ __attribute__((aligned(16))) float smem[TILE + (WLDS ? 2 * WSLAB : 0)];
+  float* const lds = smem;
 
   const int tid = threadIdx.x;
-  const int gx0 = blockIdx.x * 16;
+  const int split = NSPLIT > 1 ? (int)(blockIdx.x % NSPLIT) : 0;
+  const int gx0 = (NSPLIT > 1 ? (int)(blockIdx.x / NSPLIT) : (int)blockIdx.x) * 16;
   const int gy0 = blockIdx.y * TH;
   const int nimg = blockIdx.z;
   const int H = a.H, W = a.W;
-
-  // ---- stage the input tile (with halo) into LDS; zero outside the image (SAME pad) ----
-  for (int e = tid; e < LR * LC * C4; e += 256) {
-    const int c4 = e % C4;
-    const int pe = e / C4;
-    const int col = pe % LC;
-    const int row = pe / LC;
-    int iy, ix;
-    if constexpr (MODE == MODE_S2) {
-      const int plane = col >= 17 ? 1 : 0;
-      const int j = col - plane * 17;
-      iy = 2 * gy0 + row - a.pad_y;
-      ix = 2 * gx0 + 2 * j + plane - a.pad_x;
-    } else if constexpr (MODE == MODE_S1) {
-      iy = gy0 - a.pad_y + row;
-      ix = gx0 - a.pad_x + col;
-    } else {
-      iy = gy0 - 1 + row;
-      ix = gx0 - 1 + col;
-    }
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-      const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4;
-      if constexpr (IN == IN_F32) {
-        v = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
-      } else {
-        const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
-        v.x = a.lut[q & 0xff];
-        v.y = a.lut[(q >> 8) & 0xff];
-        v.z = a.lut[(q >> 16) & 0xff];
-        v.w = a.lut[q >> 24];
-      }
-    }
-    *reinterpret_cast<f32x4*>(&lds[(row * LC + col) * PS + c4 * 4]) = v;
-  }
-  __syncthreads();
 
   const int wave = tid >> 6;
   const int lane = tid & 63;
@@ -121,6 +106,94 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
   const int wc = wave % WC;
   const int li = lane & 15;  // pixel within the 16-pixel block (B col / D col)
   const int lg = lane >> 4;  // k group (A/B) / output channel quad (D)
+  const int co_wg = split * COUT_WG;      // first output channel of this workgroup
+  const int co_wave = wc * NB * 16;       // first channel of this wave inside the WG
+
+  // ---- weight source ----
+  auto wdma = [&](int tap, int slot) {  // LDS-DMA one tap slab: [kc][g][co_local][4]
+#pragma unroll
+    for (int j = 0; j < (WCHUNK + 255) / 256; ++j) {
+      const int cbase = (j * 4 + wave) * 64;  // wave-uniform first chunk
+      if (cbase < WCHUNK) {
+        const int c = cbase + lane;
+        const int col = c % COUT_WG, kg = c / COUT_WG;  // kg = kc*4 + g
+        const float* src = a.wp + ((size_t)(tap * KC * 4 + kg) * COUT + co_wg + col) * 4;
+        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(smem + TILE + slot * WSLAB + cbase * 4), 16, 0, 0);
+      }
+    }
+  };
+  const float* __restrict__ wl = a.wp + (size_t)(lg * COUT + co_wg + co_wave + li) * 4;
+  auto wglob = [&](int s, int nb) -> f32x4 {
+    const int tap = s / KC, kc = s % KC;
+    return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC + kc) * 4 * COUT * 4 + nb * 64);
+  };
+
+  constexpr int PF = 2;  // register prefetch distance (WLDS=false)
+  f32x4 av[WLDS ? 1 : PF + 1][NB];
+  if constexpr (WLDS) {
+    wdma(0, 0);
+  } else {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        if (p < NSTEP) av[p][nb] = wglob(p, nb);
+  }
+
+  // ---- stage the input tile (with halo) into LDS; zero outside the image (SAME pad) ----
+  // A thread's global loads are all issued before its first LDS write (batches of <= SB).
+  constexpr int NSTAGE = LR * LC * C4;
+  constexpr int NIT = (NSTAGE + 255) / 256;
+  constexpr int SB = NIT < 12 ? NIT : 12;
+#pragma unroll
+  for (int i0 = 0; i0 < NIT; i0 += SB) {
+    f32x4 tmp[SB];
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const int e = (i0 + i) * 256 + tid;
+      tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i0 + i < NIT && e < NSTAGE) {
+        const int c4 = e % C4;
+        const int pe = e / C4;
+        const int col = pe % LC;
+        const int row = pe / LC;
+        int iy, ix;
+        if constexpr (MODE == MODE_S2) {
+          const int plane = col >= 17 ? 1 : 0;
+          iy = 2 * gy0 + row - a.pad_y;
+          ix = 2 * gx0 + 2 * (col - plane * 17) + plane - a.pad_x;
+        } else if constexpr (MODE == MODE_S1) {
+          iy = gy0 - a.pad_y + row;
+          ix = gx0 - a.pad_x + col;
+        } else {
+          iy = gy0 - 1 + row;
+          ix = gx0 - 1 + col;
+        }
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+          const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4;
+          if constexpr (IN == IN_F32) {
+            tmp[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
+          } else {
+            const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
+            tmp[i].x = a.lut[q & 0xff];
+            tmp[i].y = a.lut[(q >> 8) & 0xff];
+            tmp[i].z = a.lut[(q >> 16) & 0xff];
+            tmp[i].w = a.lut[q >> 24];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const int e = (i0 + i) * 256 + tid;
+      if (i0 + i < NIT && e < NSTAGE) {
+        const int c4 = e % C4, pe = e / C4;
+        *reinterpret_cast<f32x4*>(&lds[pe * PS + c4 * 4]) = tmp[i];
+      }
+    }
+  }
+  if constexpr (WLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   f32x4 acc[NPH][MB][NB];
 #pragma unroll
@@ -130,73 +203,53 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const float* __restrict__ wp = a.wp;
-  // per-lane weight offset inside one (tap, kc) slab
-  const int wlane = ((wc * NB) * 16 + li) * 16 + lg * 4;
-
-  if constexpr (MODE != MODE_T2) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap % 3;
+  for (int s = 0; s < NSTEP; ++s) {
+    const int tap = s / KC, kc = s % KC;
+    const int ky = tap / 3, kx = tap % 3;
+    if constexpr (WLDS) {
+      if (kc == 0 && tap + 1 < 9) wdma(tap + 1, (tap + 1) & 1);
+    } else {
+      if (s + PF < NSTEP) {
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        f32x4 av[NB];
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          av[nb] = *reinterpret_cast<const f32x4*>(wp + (size_t)(tap * KC + kc) * COUT * 16 + wlane + nb * 256);
-        f32x4 bv[MB];
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const int r = wr * MB + mb;
-          int lp;
-          if constexpr (MODE == MODE_S1) lp = (r + ky) * LC + li + kx;
-          else lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
-          bv[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb) acc[0][mb][nb] = mfma4(av[nb][t], bv[mb][t], acc[0][mb][nb]);
+        for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
       }
     }
-  } else {
-    // input offsets (dy,dx) in {0,-1}^2; phase p = 2*py + px uses tap (ky,kx)
+    f32x4 aw[NB];
 #pragma unroll
-    for (int off = 0; off < 4; ++off) {
-      const int dy = -(off >> 1), dx = -(off & 1);
+    for (int nb = 0; nb < NB; ++nb) {
+      if constexpr (WLDS)
+        aw[nb] = *reinterpret_cast<const f32x4*>(
+            &smem[TILE + (tap & 1) * WSLAB + ((kc * 4 + lg) * COUT_WG + co_wave + nb * 16 + li) * 4]);
+      else
+        aw[nb] = av[s % (PF + 1)][nb];
+    }
+    int ph = 0;
+    f32x4 bv[MB];
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        f32x4 bv[MB];
+    for (int mb = 0; mb < MB; ++mb) {
+      const int r = wr * MB + mb;
+      int lp;
+      if constexpr (MODE == MODE_S1) {
+        lp = (r + ky) * LC + li + kx;
+      } else if constexpr (MODE == MODE_S2) {
+        lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
+      } else {  // T2: tap (ky,kx) feeds phase (ky==1, kx==1) from input offset (-(ky==2), -(kx==2))
+        lp = (r + 1 - (ky == 2)) * LC + li + 1 - (kx == 2);
+        ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
+      }
+      bv[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
+    }
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const int r = wr * MB + mb;
-          const int lp = (r + 1 + dy) * LC + li + 1 + dx;
-          bv[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
-        }
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int py = 0; py < 2; ++py) {
-          if (dy != 0 && py == 1) continue;
-          const int ky = py == 1 ? 1 : (dy == 0 ? 0 : 2);
+      for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-          for (int px = 0; px < 2; ++px) {
-            if (dx != 0 && px == 1) continue;
-            const int kx = px == 1 ? 1 : (dx == 0 ? 0 : 2);
-            const int tap = ky * 3 + kx;
-            f32x4 av[NB];
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-              av[nb] = *reinterpret_cast<const f32x4*>(wp + (size_t)(tap * KC + kc) * COUT * 16 + wlane + nb * 256);
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-              for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-                for (int nb = 0; nb < NB; ++nb)
-                  acc[py * 2 + px][mb][nb] = mfma4(av[nb][t], bv[mb][t], acc[py * 2 + px][mb][nb]);
-          }
-        }
+        for (int nb = 0; nb < NB; ++nb) acc[ph][mb][nb] = mfma4(aw[nb][t], bv[mb][t], acc[ph][mb][nb]);
+    if constexpr (WLDS) {
+      if (kc == KC - 1 && tap + 1 < 9) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
     }
   }
@@ -220,7 +273,7 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
       }
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        const int co = (wc * NB + nb) * 16 + lg * 4;
+        const int co = co_wg + co_wave + nb * 16 + lg * 4;
         const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + co);
         f32x4 v = acc[p][mb][nb];
         v.x = __fadd_rn(v.x, bb.x);

@@ -52,6 +52,8 @@ typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);
 struct ConvEntry {
   int mode, cin, cout, act, res, in, out;
   int th;             // output rows per block (input rows for T2)
+  int nsplit;         // workgroups splitting the output channels of one pixel tile
+  int wlds;           // weights staged through LDS by LDS-DMA (1) or read from L2 (0)
   ConvLaunch fn;
 };
 

@@ -130,31 +130,69 @@ int same_pad(int kind, int h) {
   return std::max((o - 1) * s + 3 - h, 0) / 2;
 }
 
-const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, int in, int outm) {
+// Pick a compiled tiling for this layer: the largest per-workgroup tile that still
+// gives >= 2 workgroups per CU (512 on MI355X); otherwise the variant with the most
+// workgroups.  TIC_FORCE_TILE="th,nsplit" overrides (tuning experiments).
+const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, int in, int outm, int hg = 0,
+                                int wg = 0, int n = 0) {
   const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
                                            tic::conv_registry_t2};
-  int n = 0;
-  const tic::ConvEntry* e = regs[mode](&n);
-  for (int i = 0; i < n; ++i)
-    if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
-        e[i].out == outm)
-      return &e[i];
-  return nullptr;
+  int cnt = 0;
+  const tic::ConvEntry* e = regs[mode](&cnt);
+  int fth = 0, fns = 0, fwl = -1;
+  if (const char* f = getenv("TIC_FORCE_TILE")) sscanf(f, "%d,%d,%d", &fth, &fns, &fwl);
+  const tic::ConvEntry* best = nullptr;
+  long best_wgs = -1, best_work = -1;
+  bool best_ok = false;
+  for (int i = 0; i < cnt; ++i) {
+    const tic::ConvEntry& c = e[i];
+    if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
+    if (fth && (c.th != fth || c.nsplit != fns || (fwl >= 0 && c.wlds != fwl))) continue;
+    const long wgs = (long)((wg + 15) / 16) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
+    const long work = (long)c.th * 64 / c.nsplit;  // pixels x channel-fraction per workgroup
+    const bool ok = wgs >= 512;
+    bool better;
+    if (!best) better = true;
+    else if (ok != best_ok) better = ok;
+    else if (ok) better = work > best_work || (work == best_work && wgs > best_wgs);
+    else better = wgs > best_wgs || (wgs == best_wgs && work > best_work);
+    if (better) {
+      best = &c;
+      best_wgs = wgs;
+      best_work = work;
+      best_ok = ok;
+    }
+  }
+  return best;
 }
 
-// Repack a TF kernel into the generic conv layout [tap][Cin/16][Cout][4 g][4 t].
+std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, int act, int res, int in, int outm) {
+  const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
+                                           tic::conv_registry_t2};
+  int cnt = 0;
+  const tic::ConvEntry* e = regs[mode](&cnt);
+  std::vector<const tic::ConvEntry*> out;
+  for (int i = 0; i < cnt; ++i)
+    if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
+        e[i].out == outm)
+      out.push_back(&e[i]);
+  return out;
+}
+
+// Repack a TF kernel into the generic conv layout [tap][Cin/16][4 g][Cout][4 t]
+// (input channel ci = 16 kc + 4 g + t).
 void pack_generic(const float* k, int kind, int cin, int cout, std::vector<float>* wp) {
   const int KC = cin / 16;
   wp->assign((size_t)9 * cin * cout, 0.f);
   for (int tap = 0; tap < 9; ++tap)
     for (int kc = 0; kc < KC; ++kc)
-      for (int co = 0; co < cout; ++co)
-        for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < 4; ++g)
+        for (int co = 0; co < cout; ++co)
           for (int t = 0; t < 4; ++t) {
             const int ci = kc * 16 + 4 * g + t;
             const float v = kind == K_T2 ? k[((size_t)tap * cout + co) * cin + ci]   // [kh,kw,Cout,Cin]
                                          : k[((size_t)tap * cin + ci) * cout + co];  // HWIO
-            (*wp)[((((size_t)tap * KC + kc) * cout + co) * 4 + g) * 4 + t] = v;
+            (*wp)[((((size_t)tap * KC + kc) * 4 + g) * cout + co) * 4 + t] = v;
           }
 }
 
@@ -201,6 +239,7 @@ struct LayerRT {
   float* d_w = nullptr;
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
+  std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
 };
 
 struct tic_handle {
@@ -223,6 +262,7 @@ struct tic_handle {
   void* st_out2 = nullptr;
   size_t st_out2_bytes = 0;
   std::vector<void*> user_allocs;
+  int tune_reps = 0;  // > 0 while tic_autotune runs
   bool rmbe() const { return model_id == TIC_MODEL_RMBE; }
 };
 
@@ -317,7 +357,11 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
     } else {
       const int inm = first_dec ? tic::IN_IDX : tic::IN_F32;
       const int outm = last_enc ? tic::OUT_QUANT : tic::OUT_F32;
-      const tic::ConvEntry* e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
+      const int hg = d.kind == K_T2 ? lay.h_in : lay.h_out;
+      const tic::ConvEntry* e = nullptr;
+      auto it = lay.tuned.find(n);
+      if (it != lay.tuned.end()) e = it->second;
+      else e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, hg, hg, n);
       if (!e)
         return fail(TIC_EUNSUPPORTED, "no kernel for layer %s (kind %d %d->%d act %d res %d in %d out %d)",
                     d.name.c_str(), d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
@@ -333,6 +377,32 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
       a.Ho = a.Wo = lay.h_out;
       a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
       a.qscale = (float)(h->Q - 1);
+      if (h->tune_reps > 0 && it == lay.tuned.end()) {
+        // time every compiled tiling on the live buffers (re-launching is idempotent)
+        auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
+        hipEvent_t t0, t1;
+        HIP_TRY(hipEventCreate(&t0));
+        HIP_TRY(hipEventCreate(&t1));
+        float best_ms = 1e30f;
+        for (const tic::ConvEntry* c : cands) {
+          c->fn(a, n, h->stream);  // warm
+          HIP_TRY(hipEventRecord(t0, h->stream));
+          for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, h->stream);
+          HIP_TRY(hipEventRecord(t1, h->stream));
+          HIP_TRY(hipEventSynchronize(t1));
+          float ms = 0.f;
+          HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+          if (ms < best_ms) {
+            best_ms = ms;
+            e = c;
+          }
+        }
+        (void)hipEventDestroy(t0);
+        (void)hipEventDestroy(t1);
+        int rc = check_launch();
+        if (rc) return rc;
+        lay.tuned[n] = e;
+      }
       e->fn(a, n, h->stream);
     }
     int rc = check_launch();
@@ -766,6 +836,59 @@ int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float*
   return rc;
 }
 
+int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!d_in || n <= 0 || reps <= 0) return fail(TIC_EINVAL, "bad arguments");
+  if (n > h->chunk) return fail(TIC_EINVAL, "autotune n %d exceeds chunk %d", n, h->chunk);
+  for (auto& l : h->layers) l.tuned.erase(n);
+  void *d_idx = nullptr, *d_out = nullptr;
+  const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
+  const size_t px = (size_t)n * h->P * h->P * 3;
+  HIP_TRY(hipMalloc(&d_idx, std::max<size_t>(ce, 16)));
+  HIP_TRY(hipMalloc(&d_out, px * (h->rmbe() ? 4 : 1)));
+  h->tune_reps = reps;
+  if (h->rmbe()) {
+    rc = rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr});
+  } else {
+    rc = encode_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, nullptr, Prof{nullptr});
+    if (!rc) rc = decode_dev(h, (const uint8_t*)d_idx, n, (uint8_t*)d_out, nullptr, Prof{nullptr});
+  }
+  h->tune_reps = 0;
+  hipError_t e = hipStreamSynchronize(h->stream);
+  (void)hipFree(d_idx);
+  (void)hipFree(d_out);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(TIC_EHIP, "autotune sync: %s", hipGetErrorString(e));
+  return TIC_OK;
+}
+
+int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
+  if (!h || !th || !nsplit) return fail(TIC_EINVAL, "null argument");
+  // nsplit reports (channel split) + 100 * (weights via LDS)
+  if (i < 0 || i >= (int)h->layers.size()) return fail(TIC_EINVAL, "layer index %d out of range", i);
+  *th = *nsplit = 0;
+  const LayerRT& l = h->layers[i];
+  const int L = (int)h->layers.size();
+  if (i == 0 || i == L - 1) return TIC_OK;
+  auto it = l.tuned.find(n);
+  const tic::ConvEntry* e = nullptr;
+  if (it != l.tuned.end()) {
+    e = it->second;
+  } else {
+    const LayerDef& d = l.def;
+    const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
+    const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
+    e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
+                  last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n);
+  }
+  if (e) {
+    *th = e->th;
+    *nsplit = e->nsplit + 100 * e->wlds;
+  }
+  return TIC_OK;
+}
+
 int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int n, int H, int W, int cin, int cout,
                        const float* w_host, const float* b_host, const float* d_res, float* d_out) {
   if (!h) return fail(TIC_EINVAL, "null handle");
@@ -773,7 +896,8 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
       !b_host)
     return fail(TIC_EINVAL, "bad arguments");
   HIP_TRY(hipSetDevice(h->device));
-  const tic::ConvEntry* e = find_conv(kind, cin, cout, act, d_res ? 1 : 0, tic::IN_F32, tic::OUT_F32);
+  const tic::ConvEntry* e = find_conv(kind, cin, cout, act, d_res ? 1 : 0, tic::IN_F32, tic::OUT_F32,
+                                      kind == K_T2 ? H : out_size(kind, H), kind == K_T2 ? W : out_size(kind, W), n);
   if (!e)
     return fail(TIC_EUNSUPPORTED, "no compiled conv3x3 for kind %d %d->%d act %d res %d", kind, cin, cout, act,
                 d_res ? 1 : 0);
