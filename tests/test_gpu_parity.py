@@ -140,6 +140,14 @@ def codec_std():
     return SYNTH_STD
 
 
+def test_last_layer_scatter_form(lib_codec, monkeypatch):
+    """The scatter (col2im) form of the last layer meets the same parity bar."""
+    monkeypatch.setenv("TIC_RGB_OUT_FORM", "scatter")
+    P = 64
+    codec, params = lib_codec(0, P)
+    _check_codec(codec, params, 0, P, structured_patches(3, P, seed=41))
+
+
 @pytest.mark.parametrize("model_id", [0, 1, 2, 3])
 def test_codec_small_patches(lib_codec, model_id):
     P = 64

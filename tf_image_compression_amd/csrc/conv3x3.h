@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
   const int nimg = blockIdx.z;
   const int H = a.H, W = a.W;
 
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int lane = tid & 63;
   const int wr = wave / WC;
   const int wc = wave % WC;
@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < (WCHUNK + 255) / 256; ++j) {
       const int cbase = (j * 4 + wave) * 64;  // wave-uniform first chunk
-      if (cbase < WCHUNK) {
+      if (WCHUNK % 256 == 0 || cbase < WCHUNK) {
         const int c = cbase + lane;
         const int col = c % COUT_WG, kg = c / COUT_WG;  // kg = kc*4 + g
         const float* src = a.wp + ((size_t)(tap * KC * 4 + kg) * COUT + co_wg + col) * 4;
@@ -203,10 +203,39 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fragment loaders for step s (tap-major: tap = s / KC, kc = s % KC)
+  auto load_b = [&](int s, f32x4* dst) {
+    const int tap = s / KC, kc = s % KC;
+    const int ky = tap / 3, kx = tap % 3;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int r = wr * MB + mb;
+      int lp;
+      if constexpr (MODE == MODE_S1) lp = (r + ky) * LC + li + kx;
+      else if constexpr (MODE == MODE_S2) lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
+      else lp = (r + 1 - (ky == 2)) * LC + li + 1 - (kx == 2);  // T2: input offset (-(ky==2), -(kx==2))
+      dst[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
+    }
+  };
+  auto load_a_lds = [&](int s, f32x4* dst) {
+    const int tap = s / KC, kc = s % KC;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      dst[nb] = *reinterpret_cast<const f32x4*>(
+          &smem[TILE + (tap & 1) * WSLAB + ((kc * 4 + lg) * COUT_WG + co_wave + nb * 16 + li) * 4]);
+  };
+
+  // register double buffer of the LDS fragments: step s+1's ds_reads are in flight while
+  // step s's MFMAs issue (except across a WLDS tap boundary, which needs the barrier).
+  f32x4 bq[2][MB];
+  f32x4 aq[2][WLDS ? NB : 1];
+  load_b(0, bq[0]);
+  if constexpr (WLDS) load_a_lds(0, aq[0]);
 #pragma unroll
   for (int s = 0; s < NSTEP; ++s) {
     const int tap = s / KC, kc = s % KC;
     const int ky = tap / 3, kx = tap % 3;
+    const int c = s & 1;
     if constexpr (WLDS) {
       if (kc == 0 && tap + 1 < 9) wdma(tap + 1, (tap + 1) & 1);
     } else {
@@ -215,41 +244,32 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
         for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
       }
     }
-    f32x4 aw[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      if constexpr (WLDS)
-        aw[nb] = *reinterpret_cast<const f32x4*>(
-            &smem[TILE + (tap & 1) * WSLAB + ((kc * 4 + lg) * COUT_WG + co_wave + nb * 16 + li) * 4]);
-      else
-        aw[nb] = av[s % (PF + 1)][nb];
+    const bool pre = s + 1 < NSTEP && !(WLDS && kc == KC - 1);
+    if (pre) {
+      load_b(s + 1, bq[c ^ 1]);
+      if constexpr (WLDS) load_a_lds(s + 1, aq[c ^ 1]);
     }
-    int ph = 0;
-    f32x4 bv[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const int r = wr * MB + mb;
-      int lp;
-      if constexpr (MODE == MODE_S1) {
-        lp = (r + ky) * LC + li + kx;
-      } else if constexpr (MODE == MODE_S2) {
-        lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
-      } else {  // T2: tap (ky,kx) feeds phase (ky==1, kx==1) from input offset (-(ky==2), -(kx==2))
-        lp = (r + 1 - (ky == 2)) * LC + li + 1 - (kx == 2);
-        ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
-      }
-      bv[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
-    }
+    // keep the next step's ds_reads above this step's MFMAs (hipcc otherwise sinks them
+    // below to reuse registers and then waits lgkmcnt(0) right before the next MFMAs)
+    __builtin_amdgcn_sched_barrier(0);
+    // T2: tap (ky,kx) feeds output phase 2*(ky==1) + (kx==1)
+    const int ph = MODE == MODE_T2 ? (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0) : 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) acc[ph][mb][nb] = mfma4(aw[nb][t], bv[mb][t], acc[ph][mb][nb]);
+        for (int nb = 0; nb < NB; ++nb) {
+          const float aval = WLDS ? aq[c][WLDS ? nb : 0][t] : av[s % (PF + 1)][nb][t];
+          acc[ph][mb][nb] = mfma4(aval, bq[c][mb][t], acc[ph][mb][nb]);
+        }
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (WLDS) {
       if (kc == KC - 1 && tap + 1 < 9) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        load_b(s + 1, bq[c ^ 1]);
+        load_a_lds(s + 1, aq[c ^ 1]);
       }
     }
   }
@@ -476,6 +496,145 @@ __global__ void __launch_bounds__(256) convT_rgb_kernel(const RgbOutArgs a) {
       a.out_u8[o] = (uint8_t)rintf(y[0]);
       a.out_u8[o + 1] = (uint8_t)rintf(y[1]);
       a.out_u8[o + 2] = (uint8_t)rintf(y[2]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Last layer, scatter (col2im) form: per input position (m,q) the 27 partial products
+// P[(ky,kx,co)] = sum_ci x[m,q,ci] W[ky,kx,co,ci] come from MFMA (M = 32 rows = 27 used,
+// K = Cin, N = 16 positions), land in LDS, and each output pixel (2m+py, 2q+px) sums the
+// 1, 2 or 4 partials of its phase: py=0 <- (ky=0 @ m, ky=2 @ m-1), py=1 <- (ky=1 @ m),
+// likewise in x.  The tile carries one halo row/column of positions at the top/left.
+// Then + bias, denormalise, clip, round -> u8 (and/or f32), 4 output pixels per thread.
+// Weights packed [rb 2][Cin/16][4 g][16 rows][4 t], row = 16 rb + rr = 3*tap + co.
+// ---------------------------------------------------------------------------------------
+template <int CIN, int TH>
+__global__ void __launch_bounds__(256) convT_rgb_scatter_kernel(const RgbOutArgs a) {
+  constexpr int PS = CIN + 8, KC = CIN / 16, C4 = CIN / 4;
+  constexpr int LR = TH + 1, LC = 17;
+  constexpr int NPOS = LR * LC;
+  constexpr int NPB = (NPOS + 15) / 16;
+  constexpr int PP = 36;  // partial-row stride (floats): 27 used, 16-byte aligned
+  constexpr int XT = LR * LC * PS;
+  __shared__ __attribute__((aligned(16))) float smem[XT + NPB * 16 * PP];
+  float* const part = smem + XT;
+
+  const int tid = threadIdx.x;
+  const int gx0 = blockIdx.x * 16, gy0 = blockIdx.y * TH, nimg = blockIdx.z;
+  const int H = a.H, W = a.W;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+
+  f32x4 wa[2][KC];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      wa[rb][kc] = *reinterpret_cast<const f32x4*>(a.wp2 + (((rb * KC + kc) * 4 + lg) * 16 + li) * 4);
+
+  constexpr int NSTAGE = LR * LC * C4;
+  constexpr int NIT = (NSTAGE + 255) / 256;
+  f32x4 tmp[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int e = i * 256 + tid;
+    tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e < NSTAGE) {
+      const int c4 = e % C4, pe = e / C4, col = pe % LC, row = pe / LC;
+      const int iy = gy0 - 1 + row, ix = gx0 - 1 + col;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+        tmp[i] = *reinterpret_cast<const f32x4*>(a.in + ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int e = i * 256 + tid;
+    if (e < NSTAGE) *reinterpret_cast<f32x4*>(&smem[(e / C4) * PS + (e % C4) * 4]) = tmp[i];
+  }
+  __syncthreads();
+
+  for (int pb = wave; pb < NPB; pb += 4) {
+    const int pos = pb * 16 + li;
+    f32x4 bq[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      bq[kc] = pos < NPOS ? *reinterpret_cast<const f32x4*>(&smem[pos * PS + kc * 16 + lg * 4])
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc = mfma4(wa[rb][kc][t], bq[kc][t], acc);
+      // lane holds rows 16 rb + 4 lg .. +3 of position pb*16 + li
+      *reinterpret_cast<f32x4*>(&part[pos * PP + rb * 16 + lg * 4]) = acc;
+    }
+  }
+  __syncthreads();
+
+  const int Ho = 2 * H, Wo = 2 * W;
+  constexpr int NQ = 2 * TH * 8;  // (output rows) x (quads of 4 output pixels across 32)
+  for (int it = tid; it < NQ; it += 256) {
+    const int oyl = it >> 3, quad = it & 7;
+    const int oy = 2 * gy0 + oyl;
+    const int py = oyl & 1, ml = oyl >> 1;
+    if (gy0 + ml >= H) continue;
+    float y[12];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int oxl = quad * 4 + k;
+      const int px = oxl & 1, ql = oxl >> 1;
+#pragma unroll
+      for (int co = 0; co < 3; ++co) {
+        float v;
+        if (py == 0) {
+          if (px == 0) {
+            v = part[((ml + 1) * LC + ql + 1) * PP + (0 * 3 + 0) * 3 + co];
+            v = __fadd_rn(v, part[((ml + 1) * LC + ql) * PP + (0 * 3 + 2) * 3 + co]);
+            v = __fadd_rn(v, part[(ml * LC + ql + 1) * PP + (2 * 3 + 0) * 3 + co]);
+            v = __fadd_rn(v, part[(ml * LC + ql) * PP + (2 * 3 + 2) * 3 + co]);
+          } else {
+            v = part[((ml + 1) * LC + ql + 1) * PP + (0 * 3 + 1) * 3 + co];
+            v = __fadd_rn(v, part[(ml * LC + ql + 1) * PP + (2 * 3 + 1) * 3 + co]);
+          }
+        } else {
+          if (px == 0) {
+            v = part[((ml + 1) * LC + ql + 1) * PP + (1 * 3 + 0) * 3 + co];
+            v = __fadd_rn(v, part[((ml + 1) * LC + ql) * PP + (1 * 3 + 2) * 3 + co]);
+          } else {
+            v = part[((ml + 1) * LC + ql + 1) * PP + (1 * 3 + 1) * 3 + co];
+          }
+        }
+        v = __fadd_rn(v, a.bias[co]);
+        float d = __fadd_rn(__fmul_rn(v, a.std[co]), a.mean[co]);
+        y[k * 3 + co] = fminf(fmaxf(d, 0.f), 255.f);
+      }
+    }
+    const int ox0 = 2 * gx0 + quad * 4;
+    if (ox0 >= Wo) continue;
+    const size_t o = ((size_t)(nimg * Ho + oy) * Wo + ox0) * 3;
+    const bool full = ox0 + 4 <= Wo;
+    if (a.out_f32) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k)
+        if (full || ox0 + k / 3 < Wo) a.out_f32[o + k] = y[k];
+    }
+    if (a.out_u8) {
+      uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 12; ++k) w[k >> 2] |= (uint32_t)rintf(y[k]) << (8 * (k & 3));
+      if (full && (o & 3) == 0) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(a.out_u8 + o);
+        d[0] = w[0];
+        d[1] = w[1];
+        d[2] = w[2];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+          if (ox0 + k / 3 < Wo) a.out_u8[o + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+      }
     }
   }
 }

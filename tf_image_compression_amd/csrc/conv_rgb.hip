@@ -1,33 +1,70 @@
 // First layer (u8/f32 RGB -> normalise -> stride-2 conv) and last layer
-// (transpose conv -> denormalise -> clip -> round -> u8) of every codec.
+// (transpose conv -> denormalise -> clip -> round -> u8) of every codec, with their
+// tiling variants (selected per layer by tic_autotune).
 #include "conv3x3.h"
 
 namespace tic {
 
-bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s) {
-  constexpr int TH = 4;
+int rgb_in_variants() { return 3; }  // TH = 4, 8, 16 output rows per workgroup
+
+template <int COUT, int TH>
+static bool rgb_in_th(bool u8_input, const RgbInArgs& a, int n, hipStream_t s) {
   dim3 grid((a.Wo + 15) / 16, (a.Ho + TH - 1) / TH, n);
-  if (cout == 32 && u8_input)
-    hipLaunchKernelGGL((conv_rgb_s2_kernel<32, TH, true>), grid, dim3(256), 0, s, a);
-  else if (cout == 16 && u8_input)
-    hipLaunchKernelGGL((conv_rgb_s2_kernel<16, TH, true>), grid, dim3(256), 0, s, a);
-  else if (cout == 32 && !u8_input)
-    hipLaunchKernelGGL((conv_rgb_s2_kernel<32, TH, false>), grid, dim3(256), 0, s, a);
+  if (u8_input)
+    hipLaunchKernelGGL((conv_rgb_s2_kernel<COUT, TH, true>), grid, dim3(256), 0, s, a);
   else
-    return false;
+    hipLaunchKernelGGL((conv_rgb_s2_kernel<COUT, TH, false>), grid, dim3(256), 0, s, a);
   return true;
 }
 
-bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s) {
-  constexpr int TH = 4;
+template <int COUT>
+static bool rgb_in_c(bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant) {
+  switch (variant) {
+    case 0: return rgb_in_th<COUT, 4>(u8_input, a, n, s);
+    case 1: return rgb_in_th<COUT, 8>(u8_input, a, n, s);
+    case 2: return rgb_in_th<COUT, 16>(u8_input, a, n, s);
+  }
+  return false;
+}
+
+bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant) {
+  if (cout == 32) return rgb_in_c<32>(u8_input, a, n, s, variant);
+  if (cout == 16) return rgb_in_c<16>(u8_input, a, n, s, variant);
+  return false;
+}
+
+// Variants 0-2: dense sub-pixel form, TH 4/8/16 (one summation order: autotuned).
+// Variants 3-5: scatter form, TH 4/8/16 (different tap summation order; chosen only via
+// TIC_RGB_OUT_FORM=scatter so that tuning never changes results).
+int rgb_out_variants() { return 3; }
+
+template <int CIN, int TH, bool SCATTER>
+static bool rgb_out_th(const RgbOutArgs& a, int n, hipStream_t s) {
   dim3 grid((a.W + 15) / 16, (a.H + TH - 1) / TH, n);
-  if (cin == 32)
-    hipLaunchKernelGGL((convT_rgb_kernel<32, TH>), grid, dim3(256), 0, s, a);
-  else if (cin == 16)
-    hipLaunchKernelGGL((convT_rgb_kernel<16, TH>), grid, dim3(256), 0, s, a);
+  if (SCATTER)
+    hipLaunchKernelGGL((convT_rgb_scatter_kernel<CIN, TH>), grid, dim3(256), 0, s, a);
   else
-    return false;
+    hipLaunchKernelGGL((convT_rgb_kernel<CIN, TH>), grid, dim3(256), 0, s, a);
   return true;
+}
+
+template <int CIN>
+static bool rgb_out_c(const RgbOutArgs& a, int n, hipStream_t s, int variant) {
+  switch (variant) {
+    case 0: return rgb_out_th<CIN, 4, false>(a, n, s);
+    case 1: return rgb_out_th<CIN, 8, false>(a, n, s);
+    case 2: return rgb_out_th<CIN, 16, false>(a, n, s);
+    case 3: return rgb_out_th<CIN, 4, true>(a, n, s);
+    case 4: return rgb_out_th<CIN, 8, true>(a, n, s);
+    case 5: return rgb_out_th<CIN, 16, true>(a, n, s);
+  }
+  return false;
+}
+
+bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant) {
+  if (cin == 32) return rgb_out_c<32>(a, n, s, variant);
+  if (cin == 16) return rgb_out_c<16>(a, n, s, variant);
+  return false;
 }
 
 }  // namespace tic

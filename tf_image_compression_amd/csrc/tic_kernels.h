@@ -39,7 +39,8 @@ struct RgbInArgs {
 
 struct RgbOutArgs {
   const float* in;     // [N,H,W,Cin]
-  const float* wp;     // [4 off][Cin/16][16 rows][4][4]
+  const float* wp;     // dense sub-pixel form: [4 off][Cin/16][16 rows][4][4]
+  const float* wp2;    // scatter form: [2 rb][Cin/16][4 g][16 rows][4 t]
   const float* bias;   // [3]
   uint8_t* out_u8;     // [N,2H,2W,3] or nullptr
   float* out_f32;      // [N,2H,2W,3] or nullptr
@@ -62,8 +63,11 @@ const ConvEntry* conv_registry_s1(int* count);
 const ConvEntry* conv_registry_s2(int* count);
 const ConvEntry* conv_registry_t2(int* count);
 
-// First / last layer launchers (conv_rgb.hip); return false if the width is not compiled.
-bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s);
-bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s);
+// First / last layer launchers (conv_rgb.hip); `variant` < rgb_*_variants() selects the
+// tiling / formulation; return false if the width is not compiled.
+int rgb_in_variants();
+int rgb_out_variants();
+bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant);
+bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant);
 
 }  // namespace tic

@@ -13,6 +13,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -230,6 +231,22 @@ void pack_rgb_out(const float* k, int cin, std::vector<float>* wp) {
   }
 }
 
+// Last layer, scatter form: [2 rb][Cin/16][4 g][16 rows][4 t], row 16 rb + rr = 3 tap + co.
+void pack_rgb_out_scatter(const float* k, int cin, std::vector<float>* wp) {
+  const int KC = cin / 16;
+  wp->assign((size_t)2 * cin * 16, 0.f);
+  for (int rb = 0; rb < 2; ++rb)
+    for (int rr = 0; rr < 16; ++rr) {
+      const int row = rb * 16 + rr;
+      if (row >= 27) continue;
+      const int tap = row / 3, co = row % 3;
+      for (int ci = 0; ci < cin; ++ci) {
+        const int kc = ci / 16, g = (ci % 16) / 4, t = ci % 4;
+        (*wp)[((((size_t)rb * KC + kc) * 4 + g) * 16 + rr) * 4 + t] = k[((size_t)tap * 3 + co) * cin + ci];
+      }
+    }
+}
+
 }  // namespace
 
 struct LayerRT {
@@ -237,9 +254,11 @@ struct LayerRT {
   std::vector<float> k, b;
   bool has_k = false, has_b = false;
   float* d_w = nullptr;
+  float* d_w2 = nullptr;  // alternate packing (last layer: scatter form)
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
+  std::map<int, int> tuned_var;                 // first/last layer: batch size -> variant
 };
 
 struct tic_handle {
@@ -296,6 +315,42 @@ int check_launch() {
   return TIC_OK;
 }
 
+// Time `nvar` launch variants (reps each, after one warm launch) and return the fastest.
+int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(int)>& launch, int* best) {
+  hipEvent_t t0, t1;
+  HIP_TRY(hipEventCreate(&t0));
+  HIP_TRY(hipEventCreate(&t1));
+  float best_ms = 1e30f;
+  *best = -1;
+  for (int v = 0; v < nvar; ++v) {
+    if (!launch(v)) continue;
+    HIP_TRY(hipEventRecord(t0, st));
+    for (int r = 0; r < reps; ++r) launch(v);
+    HIP_TRY(hipEventRecord(t1, st));
+    HIP_TRY(hipEventSynchronize(t1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+    if (ms < best_ms) {
+      best_ms = ms;
+      *best = v;
+    }
+  }
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(TIC_EHIP, "tuning launch failed: %s", hipGetErrorString(e));
+  if (*best < 0) return fail(TIC_EUNSUPPORTED, "no launchable variant");
+  return TIC_OK;
+}
+
+const int kRgbInDefault = 2;   // TH 16
+const int kRgbOutDefault = 0;  // dense sub-pixel form, TH 4
+
+int rgb_out_forced() {  // TIC_RGB_OUT_FORM=scatter -> scatter form TH 8 (experiments/tests)
+  const char* f = getenv("TIC_RGB_OUT_FORM");
+  return (f && std::string(f) == "scatter") ? 4 : -1;
+}
+
 struct Prof {
   hipEvent_t* ev;  // 2 per layer, or nullptr
 };
@@ -338,12 +393,21 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
         a.mean[c] = h->mean[c];
         a.std[c] = h->std[c];
       }
-      if (!tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, h->stream))
+      auto it = lay.tuned_var.find(n);
+      int var = it != lay.tuned_var.end() ? it->second : kRgbInDefault;
+      if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
+        int rc = time_variants(h->stream, tic::rgb_in_variants(), h->tune_reps,
+                               [&](int v) { return tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, h->stream, v); }, &var);
+        if (rc) return rc;
+        lay.tuned_var[n] = var;
+      }
+      if (!tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, h->stream, var))
         return fail(TIC_EUNSUPPORTED, "first layer %s: width %d not compiled", d.name.c_str(), d.cout);
     } else if (last) {
       tic::RgbOutArgs a{};
       a.in = src;
       a.wp = lay.d_w;
+      a.wp2 = lay.d_w2;
       a.bias = lay.d_b;
       a.out_u8 = d_rgb;
       a.out_f32 = d_f32;
@@ -352,7 +416,17 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
         a.mean[c] = h->mean[c];
         a.std[c] = h->std[c];
       }
-      if (!tic::launch_rgb_out(d.cin, a, n, h->stream))
+      auto it = lay.tuned_var.find(n);
+      int var = it != lay.tuned_var.end() ? it->second : kRgbOutDefault;
+      const int forced = rgb_out_forced();
+      if (forced >= 0) var = forced;
+      else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
+        int rc = time_variants(h->stream, tic::rgb_out_variants(), h->tune_reps,
+                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, h->stream, v); }, &var);
+        if (rc) return rc;
+        lay.tuned_var[n] = var;
+      }
+      if (!tic::launch_rgb_out(d.cin, a, n, h->stream, var))
         return fail(TIC_EUNSUPPORTED, "last layer %s: width %d not compiled", d.name.c_str(), d.cin);
     } else {
       const int inm = first_dec ? tic::IN_IDX : tic::IN_F32;
@@ -556,6 +630,7 @@ void tic_destroy(tic_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (auto& l : h->layers) {
     if (l.d_w) (void)hipFree(l.d_w);
+    if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   for (auto& b : h->ws)
@@ -628,8 +703,15 @@ int tic_finalize(tic_handle* h) {
     else if (i == L - 1) pack_rgb_out(l.k.data(), l.def.cin, &wp);
     else pack_generic(l.k.data(), l.def.kind, l.def.cin, l.def.cout, &wp);
     if (l.d_w) (void)hipFree(l.d_w);
+    if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_b) (void)hipFree(l.d_b);
-    l.d_w = l.d_b = nullptr;
+    l.d_w = l.d_w2 = l.d_b = nullptr;
+    if (i == L - 1) {
+      std::vector<float> w2;
+      pack_rgb_out_scatter(l.k.data(), l.def.cin, &w2);
+      HIP_TRY(hipMalloc((void**)&l.d_w2, w2.size() * sizeof(float)));
+      HIP_TRY(hipMemcpy(l.d_w2, w2.data(), w2.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMalloc((void**)&l.d_w, wp.size() * sizeof(float)));
     HIP_TRY(hipMemcpy(l.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc((void**)&l.d_b, std::max<size_t>(l.b.size(), 16) * sizeof(float)));
@@ -841,7 +923,10 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
   if (rc) return rc;
   if (!d_in || n <= 0 || reps <= 0) return fail(TIC_EINVAL, "bad arguments");
   if (n > h->chunk) return fail(TIC_EINVAL, "autotune n %d exceeds chunk %d", n, h->chunk);
-  for (auto& l : h->layers) l.tuned.erase(n);
+  for (auto& l : h->layers) {
+    l.tuned.erase(n);
+    l.tuned_var.erase(n);
+  }
   void *d_idx = nullptr, *d_out = nullptr;
   const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
   const size_t px = (size_t)n * h->P * h->P * 3;
@@ -870,7 +955,14 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
   *th = *nsplit = 0;
   const LayerRT& l = h->layers[i];
   const int L = (int)h->layers.size();
-  if (i == 0 || i == L - 1) return TIC_OK;
+  if (i == 0 || i == L - 1) {
+    auto iv = l.tuned_var.find(n);
+    const int v = iv != l.tuned_var.end() ? iv->second : (i == 0 ? kRgbInDefault : kRgbOutDefault);
+    static const int th_in[3] = {4, 8, 16}, th_out[6] = {4, 8, 16, 4, 8, 16};
+    *th = i == 0 ? th_in[v] : th_out[v];
+    *nsplit = (i == L - 1 && v >= 3) ? 1 : 0;  // last layer: 1 = scatter form
+    return TIC_OK;
+  }
   auto it = l.tuned.find(n);
   const tic::ConvEntry* e = nullptr;
   if (it != l.tuned.end()) {
