@@ -7,7 +7,7 @@ BUILD    := build
 LIB      := tf_image_compression_amd/libtic.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)
 KERNELS  := conv_s1 conv_s2 conv_t2 conv_rgb
-OBJS     := $(addprefix $(BUILD)/,$(addsuffix .o,$(KERNELS))) $(BUILD)/tic_runtime.o
+OBJS     := $(addprefix $(BUILD)/,$(addsuffix .o,$(KERNELS))) $(BUILD)/tic_runtime.o $(BUILD)/range_coder.o
 HDRS     := $(wildcard $(CSRC)/*.h) include/tic.h
 
 all: $(LIB)
@@ -17,6 +17,9 @@ $(BUILD)/%.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
 
 $(BUILD)/tic_runtime.o: $(CSRC)/tic_runtime.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(BUILD)/range_coder.o: $(CSRC)/range_coder.cpp include/tic.h | $(BUILD)
+	g++ -O2 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-rpath,/opt/rocm/lib

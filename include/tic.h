@@ -31,6 +31,8 @@ extern "C" {
 #define TIC_EHIP (-4)       /* HIP runtime error */
 #define TIC_ENOMEM (-5)
 #define TIC_EUNSUPPORTED (-6)
+#define TIC_EOVERFLOW (-7)  /* value does not fit (reference: OverflowError) */
+#define TIC_EIO (-8)        /* file I/O (reference: IOError / RuntimeError) */
 
 #define TIC_MODEL_RMBE 100  /* submit/2/rmbe/model.py:113 (block-effect post-filter) */
 
@@ -133,6 +135,25 @@ int tic_get_stream(tic_handle* h, void** stream);
 
 /* Device info string (name, CUs, arch) for logs. */
 int tic_device_info(tic_handle* h, char* buf, int len);
+
+/* --- entropy coder (host, no device) ---
+ * Replaces the third-party `range_coder` package used by encode.py:86-97 and
+ * decode.py:89-99: RangeEncoder(path).encode(data, cum_freq) / .close() and
+ * RangeDecoder(path).decode(n, cum_freq) / .close().  cum_freq: non-decreasing int64
+ * table starting at 0, entries < 2^32 (else TIC_EOVERFLOW), total <= 2^24.  Symbols
+ * with zero frequency or outside the table are TIC_EINVAL; calls after close are
+ * TIC_ESTATE.  Several encode() calls append to one stream. */
+typedef struct tic_rc_encoder tic_rc_encoder;
+typedef struct tic_rc_decoder tic_rc_decoder;
+const char* tic_rc_last_error(void);
+int tic_rc_encoder_open(const char* path, tic_rc_encoder** out);
+int tic_rc_encode(tic_rc_encoder* e, const int64_t* data, size_t n, const int64_t* cum_freq, size_t ncum);
+int tic_rc_encoder_close(tic_rc_encoder* e);
+void tic_rc_encoder_free(tic_rc_encoder* e);
+int tic_rc_decoder_open(const char* path, tic_rc_decoder** out);
+int tic_rc_decode(tic_rc_decoder* d, size_t n, const int64_t* cum_freq, size_t ncum, int64_t* out);
+int tic_rc_decoder_close(tic_rc_decoder* d);
+void tic_rc_decoder_free(tic_rc_decoder* d);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TIC_LIB", os.path.join(_HERE, "libtic.so"))
 
 TIC_OK = 0
-ERRORS = {-1: "EINVAL", -2: "ENOTFOUND", -3: "ESTATE", -4: "EHIP", -5: "ENOMEM", -6: "EUNSUPPORTED"}
+ERRORS = {-1: "EINVAL", -2: "ENOTFOUND", -3: "ESTATE", -4: "EHIP", -5: "ENOMEM", -6: "EUNSUPPORTED",
+          -7: "EOVERFLOW", -8: "EIO"}
 TIC_MODEL_RMBE = 100
 
 u8p = C.POINTER(C.c_uint8)
@@ -53,6 +54,16 @@ SIGNATURES = [
     ("tic_conv3x3_device", C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      f32p, f32p, vp, vp]),
     ("tic_get_stream", C.c_int, [vp, C.POINTER(vp)]),
+    # entropy coder (host only)
+    ("tic_rc_last_error", C.c_char_p, []),
+    ("tic_rc_encoder_open", C.c_int, [C.c_char_p, C.POINTER(vp)]),
+    ("tic_rc_encode", C.c_int, [vp, C.POINTER(C.c_int64), C.c_size_t, C.POINTER(C.c_int64), C.c_size_t]),
+    ("tic_rc_encoder_close", C.c_int, [vp]),
+    ("tic_rc_encoder_free", None, [vp]),
+    ("tic_rc_decoder_open", C.c_int, [C.c_char_p, C.POINTER(vp)]),
+    ("tic_rc_decode", C.c_int, [vp, C.c_size_t, C.POINTER(C.c_int64), C.c_size_t, C.POINTER(C.c_int64)]),
+    ("tic_rc_decoder_close", C.c_int, [vp]),
+    ("tic_rc_decoder_free", None, [vp]),
     ("tic_device_info", C.c_int, [vp, C.c_char_p, C.c_int]),
 ]
 
