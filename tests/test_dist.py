@@ -1,0 +1,70 @@
+"""Multi-rank path on CPU: static sharding, the stats all-gather (gloo, world size 2, the
+same orchestration code the RCCL path runs), the unique-id bootstrap, and the dataset
+metrics against a single-process computation (processing_utils/evaluate.py formula)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import tic_oracle as o
+from tf_image_compression_amd import dist, sharded
+
+
+@pytest.mark.parametrize("n,world", [(10, 2), (10000, 8), (7, 8), (0, 3), (1250, 1)])
+def test_shard_range_partitions(n, world):
+    seen = []
+    for r in range(world):
+        lo, hi = dist.shard_range(n, r, world)
+        assert 0 <= lo <= hi <= n
+        seen.extend(range(lo, hi))
+    assert seen == list(range(n))
+
+
+def test_combine_matches_dataset_psnr():
+    r = np.random.default_rng(0)
+    a = [r.integers(0, 256, (8, 9, 3), dtype=np.uint8) for _ in range(5)]
+    b = [np.clip(x.astype(int) + r.integers(-5, 6, x.shape), 0, 255).astype(np.uint8) for x in a]
+    sts = []
+    for k in range(5):
+        s = dist.RankStats(sse=float(np.sum((a[k].astype(float) - b[k]) ** 2)), dims=a[k].size, bits=100,
+                           images=1, t_start=k, t_end=k + 1)
+        sts.append(dist.RankStats.from_array(s.to_array()))
+    res = dist.combine(sts)
+    assert abs(res["psnr_db"] - o.dataset_psnr(list(zip(a, b)))) < 1e-9
+    assert res["images"] == 5 and abs(res["bpp"] - 500 / (5 * 72)) < 1e-12 and res["seconds"] == 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gloo_world2_sharded_stats(tmp_path):
+    n, P = 7, 32
+    port = _free_port()
+    out = str(tmp_path / "res")
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "dist_worker.py"),
+           out, str(n), str(P)]
+    subprocess.run(cmd, check=True, env=env, timeout=240, cwd=ROOT)
+    res = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    assert res[0]["summary"] == res[1]["summary"]
+    assert res[0]["images"] == [4, 3] and all(x["uid_ok"] for x in res) and res[0]["tmax"] == 2.0
+    # single-process reference over the whole set
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    params = synthetic_params(1)
+    x = sharded.image_batch(0, n, P)
+    _, idx = o.encoder(params, SYNTH_MEAN, SYNTH_STD, x, P, 2, 1)
+    y = o.decoder(params, SYNTH_MEAN, SYNTH_STD, idx, 2, 1)[1]
+    psnr = o.dataset_psnr(list(zip(x, y)))
+    assert abs(res[0]["summary"]["psnr_db"] - psnr) < 1e-6
+    assert res[0]["summary"]["bpp"] == pytest.approx(0.25)

@@ -124,9 +124,10 @@ class RangeDecoder:
 def prob_to_cum_freq(prob, resolution=1024):
     """Probability vector -> cumulative frequency table [0, ..., resolution] in which every
     non-zero probability gets a non-zero frequency and zero probabilities get none
-    (properties pinned by other/test_range_coder.py:186-229).  Frequencies are the rounded-
-    down shares of the remaining mass after one count per non-zero symbol; the leftover
-    counts go to the largest fractional remainders (ties to the lower index)."""
+    (properties pinned by other/test_range_coder.py:186-229).  Frequencies are
+    floor(p * resolution), raised to 1 for every non-zero p; missing counts go to the
+    largest fractional remainders (ties to the lower index), surplus counts are taken from
+    the entries rounded up the most.  The package's exact rounding is unvendored."""
     p = np.asarray(prob, dtype=np.float64).reshape(-1)
     if p.size == 0 or np.any(p < 0) or not np.all(np.isfinite(p)) or p.sum() <= 0:
         raise ValueError("invalid probability vector")
