@@ -99,6 +99,13 @@ int tic_decode_device(tic_handle* h, const uint8_t* d_idx, int n, uint8_t* d_rgb
 int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, uint8_t* d_rgb);
 int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out);
 
+/* Options: "streams" (1 or 2 execution lanes; with 2, every batch chunk is split in halves
+ * on two HIP streams that run concurrently — default 2, env TIC_STREAMS), "chunk" (max
+ * patches per launch sequence, default 256, env TIC_MAX_CHUNK), "graph" (1: replay
+ * tic_codec_device as a captured HIP graph per (buffers, n) — default 0: measured slower
+ * than eager dual-lane launches on MI355X). */
+int tic_set_option(tic_handle* h, const char* key, int value);
+
 /* --- introspection / measurement --- */
 int tic_num_layers(const tic_handle* h);
 /* kind: 0 conv s1, 1 conv s2, 2 conv-transpose s2; act: 0 identity, 1 relu;

@@ -37,7 +37,7 @@ def lib_codec():
         c.close()
 
 
-TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1)] for wl in (0, 1)]
+TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1)] for wl in (0, 1, 2)]
 
 LAYER_CASES = [
     (K_S1, 64, 64, 1, False, 16, 16),
@@ -198,6 +198,32 @@ def test_autotuned_equals_default(lib_codec):
     assert np.array_equal(d_rgb.download(x.shape, np.uint8), ref_rgb)
     for b in (d_in, d_idx, d_pre, d_rgb):
         b.free()
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 256), (1, 64), (3, 128), (2, 64)])
+def test_fused_first_layers_bit_identical(lib_codec, model_id, P):
+    """enc01_kernel (layers 0+1 through LDS) == the two separate kernels, bit for bit."""
+    codec, params = lib_codec(model_id, P)
+    x = structured_patches(5, P, seed=50 + model_id)
+    codec.set_option("fuse01", 0)
+    idx0, pre0 = codec.encode(x, return_preact=True)
+    codec.set_option("fuse01", 1)
+    idx1, pre1 = codec.encode(x, return_preact=True)
+    assert np.array_equal(pre0, pre1) and np.array_equal(idx0, idx1)
+
+
+def test_fused_rmbe_first_layers_bit_identical():
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import RMBE_ID
+    r = np.random.default_rng(4)
+    win = np.clip(r.normal(120, 50, (3, 128, 128, 3)), 0, 255).astype(np.float32)
+    with Codec(RMBE_ID, synthetic_params(RMBE_ID), SYNTH_MEAN, SYNTH_STD, patch_size=128) as c:
+        c.set_option("fuse01", 0)
+        a = c.rmbe_windows(win)
+        c.set_option("fuse01", 1)
+        b = c.rmbe_windows(win)
+    assert np.array_equal(a, b)
 
 
 def test_quan_scale_256(lib_codec):

@@ -44,6 +44,7 @@ SIGNATURES = [
     ("tic_decode_device", C.c_int, [vp, vp, C.c_int, vp, vp]),
     ("tic_codec_device", C.c_int, [vp, vp, C.c_int, vp, vp]),
     ("tic_rmbe_device", C.c_int, [vp, vp, C.c_int, vp]),
+    ("tic_set_option", C.c_int, [vp, C.c_char_p, C.c_int]),
     ("tic_num_layers", C.c_int, [vp]),
     ("tic_layer_info", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p, i32p, i32p, i32p]),
     ("tic_model_num_layers", C.c_int, [C.c_int]),

@@ -164,6 +164,9 @@ class Codec:
     def rmbe_device(self, d_in: DeviceBuffer, n: int, d_out: DeviceBuffer):
         check(lib().tic_rmbe_device(self._h, d_in.ptr, n, d_out.ptr), "tic_rmbe_device")
 
+    def set_option(self, key: str, value: int) -> None:
+        check(lib().tic_set_option(self._h, key.encode(), int(value)), f"tic_set_option({key})")
+
     def stream_ptr(self) -> C.c_void_p:
         s = C.c_void_p()
         check(lib().tic_get_stream(self._h, C.byref(s)), "tic_get_stream")

@@ -328,6 +328,218 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Persistent loader/consumer variant of conv3x3_kernel (same tiling, same tap-major fma
+// order -> bit-identical results).  320 threads: waves 0-3 compute exactly as above, wave 4
+// only moves data — it stages tile i+1's input (with halo) into the other half of a
+// double-buffered LDS tile while the compute waves run tile i.  vmcnt is per wave, so the
+// compute waves' weight-fragment waits never wait on the loader's global loads.  Each
+// workgroup walks tiles blockIdx.x, blockIdx.x + gridDim.x, ...  (grid = min(tiles,
+// CUs x resident workgroups)).
+// ---------------------------------------------------------------------------------------
+template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, int ACT, bool RES, int IN, int OUT>
+__global__ void __launch_bounds__(320) conv3x3_pipe_kernel(const ConvArgs a, int ntx, int nty, int ntiles) {
+  constexpr int PS = CIN + 8;
+  constexpr int KC = CIN / 16;
+  constexpr int COUT_WG = COUT / NSPLIT;
+  constexpr int NBT = COUT_WG / 16;
+  constexpr int WC = 4 / WR;
+  static_assert(WR * WC == 4 && TH % WR == 0 && NBT % WC == 0, "bad wave split");
+  constexpr int NB = NBT / WC;
+  constexpr int MB = TH / WR;
+  constexpr int NPH = MODE == MODE_T2 ? 4 : 1;
+  constexpr int LR = TileGeom<MODE, TH>::LR;
+  constexpr int LC = TileGeom<MODE, TH>::LC;
+  constexpr int C4 = CIN / 4;
+  constexpr int NSTEP = 9 * KC;
+  constexpr int TILE = LR * LC * PS;
+  constexpr int NSTAGE = LR * LC * C4;
+  __shared__ __attribute__((aligned(16))) float smem[2 * TILE];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int H = a.H, W = a.W;
+
+  auto decode_tile = [&](int t, int& split, int& gx0, int& gy0, int& nimg) {
+    split = t % NSPLIT;
+    int r = t / NSPLIT;
+    gx0 = (r % ntx) * 16;
+    r /= ntx;
+    gy0 = (r % nty) * TH;
+    nimg = r / nty;
+  };
+  // loader wave: global -> registers (batches of 16 float4 per lane) -> LDS buffer
+  auto load_tile = [&](int t, float* dst) {
+    int split, gx0, gy0, nimg;
+    decode_tile(t, split, gx0, gy0, nimg);
+    constexpr int NIT = (NSTAGE + 63) / 64;
+    constexpr int SB = NIT < 16 ? NIT : 16;
+#pragma unroll
+    for (int i0 = 0; i0 < NIT; i0 += SB) {
+      f32x4 tmp[SB];
+#pragma unroll
+      for (int i = 0; i < SB; ++i) {
+        const int e = (i0 + i) * 64 + lane;
+        tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (i0 + i < NIT && e < NSTAGE) {
+          const int c4 = e % C4, pe = e / C4, col = pe % LC, row = pe / LC;
+          int iy, ix;
+          if constexpr (MODE == MODE_S2) {
+            const int plane = col >= 17 ? 1 : 0;
+            iy = 2 * gy0 + row - a.pad_y;
+            ix = 2 * gx0 + 2 * (col - plane * 17) + plane - a.pad_x;
+          } else if constexpr (MODE == MODE_S1) {
+            iy = gy0 - a.pad_y + row;
+            ix = gx0 - a.pad_x + col;
+          } else {
+            iy = gy0 - 1 + row;
+            ix = gx0 - 1 + col;
+          }
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+            const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4;
+            if constexpr (IN == IN_F32) {
+              tmp[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
+            } else {
+              const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
+              tmp[i].x = a.lut[q & 0xff];
+              tmp[i].y = a.lut[(q >> 8) & 0xff];
+              tmp[i].z = a.lut[(q >> 16) & 0xff];
+              tmp[i].w = a.lut[q >> 24];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < SB; ++i) {
+        const int e = (i0 + i) * 64 + lane;
+        if (i0 + i < NIT && e < NSTAGE) *reinterpret_cast<f32x4*>(&dst[(e / C4) * PS + (e % C4) * 4]) = tmp[i];
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (wave == 4 && t < ntiles) load_tile(t, smem);
+  __syncthreads();
+
+  const int wr = (wave & 3) / WC, wc = (wave & 3) % WC;
+  const int li = lane & 15, lg = lane >> 4;
+  const int co_wave = wc * NB * 16;
+  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+    float* const lds = smem + (it & 1) * TILE;
+    if (wave == 4) {
+      if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x, smem + ((it + 1) & 1) * TILE);
+    } else {
+      int split, gx0, gy0, nimg;
+      decode_tile(t, split, gx0, gy0, nimg);
+      const int co_wg = split * COUT_WG;
+      const float* __restrict__ wl = a.wp + (size_t)(lg * COUT + co_wg + co_wave + li) * 4;
+      auto wglob = [&](int s, int nb) -> f32x4 {
+        const int tap = s / KC, kc = s % KC;
+        return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC + kc) * 4 * COUT * 4 + nb * 64);
+      };
+      constexpr int PF = 2;
+      f32x4 av[PF + 1][NB];
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) av[p][nb] = wglob(p, nb);
+      auto load_b = [&](int s, f32x4* dst) {
+        const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const int r = wr * MB + mb;
+          int lp;
+          if constexpr (MODE == MODE_S1) lp = (r + ky) * LC + li + kx;
+          else if constexpr (MODE == MODE_S2) lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
+          else lp = (r + 1 - (ky == 2)) * LC + li + 1 - (kx == 2);
+          dst[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
+        }
+      };
+      f32x4 acc[NPH][MB][NB];
+#pragma unroll
+      for (int p = 0; p < NPH; ++p)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 bq[2][MB];
+      load_b(0, bq[0]);
+#pragma unroll
+      for (int s = 0; s < NSTEP; ++s) {
+        const int tap = s / KC, ky = tap / 3, kx = tap % 3;
+        const int c = s & 1;
+        if (s + PF < NSTEP) {
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
+        }
+        if (s + 1 < NSTEP) load_b(s + 1, bq[c ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const int ph = MODE == MODE_T2 ? (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0) : 0;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+              acc[ph][mb][nb] = mfma4(av[s % (PF + 1)][nb][tt], bq[c][mb][tt], acc[ph][mb][nb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int Ho = a.Ho, Wo = a.Wo;
+#pragma unroll
+      for (int p = 0; p < NPH; ++p) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const int r = wr * MB + mb;
+          int oy, ox;
+          if constexpr (MODE == MODE_T2) {
+            if (gy0 + r >= H || gx0 + li >= W) continue;
+            oy = 2 * (gy0 + r) + (p >> 1);
+            ox = 2 * (gx0 + li) + (p & 1);
+          } else {
+            oy = gy0 + r;
+            ox = gx0 + li;
+            if (oy >= Ho || ox >= Wo) continue;
+          }
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const int co = co_wg + co_wave + nb * 16 + lg * 4;
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + co);
+            f32x4 v = acc[p][mb][nb];
+            v.x = __fadd_rn(v.x, bb.x);
+            v.y = __fadd_rn(v.y, bb.y);
+            v.z = __fadd_rn(v.z, bb.z);
+            v.w = __fadd_rn(v.w, bb.w);
+            if constexpr (ACT == ACT_RELU) {
+              v.x = fmaxf(v.x, 0.f);
+              v.y = fmaxf(v.y, 0.f);
+              v.z = fmaxf(v.z, 0.f);
+              v.w = fmaxf(v.w, 0.f);
+            }
+            const size_t o = ((size_t)(nimg * Ho + oy) * Wo + ox) * COUT + co;
+            if constexpr (RES) {
+              const f32x4 rr = *reinterpret_cast<const f32x4*>(a.res + o);
+              v.x = __fadd_rn(v.x, rr.x);
+              v.y = __fadd_rn(v.y, rr.y);
+              v.z = __fadd_rn(v.z, rr.z);
+              v.w = __fadd_rn(v.w, rr.w);
+            }
+            if constexpr (OUT == OUT_F32) {
+              *reinterpret_cast<f32x4*>(a.out + o) = v;
+            } else {
+              if (a.out) *reinterpret_cast<f32x4*>(a.out + o) = v;
+              const uint32_t q = quant1(v.x, a.qscale) | (quant1(v.y, a.qscale) << 8) |
+                                 (quant1(v.z, a.qscale) << 16) | (quant1(v.w, a.qscale) << 24);
+              *reinterpret_cast<uint32_t*>(a.qout + o) = q;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // First layer: stride-2 3x3 conv from 3-channel RGB (u8 or f32) with the normalisation
 // (x - mean) / std (model_0/model.py:44) fused into the LDS staging.  K = 27 (+1 zero)
 // = 7 MFMA k-steps; lane group g supplies k = 4t + g -> (tap, channel) = divmod(k, 3).
@@ -635,6 +847,217 @@ __global__ void __launch_bounds__(256) convT_rgb_scatter_kernel(const RgbOutArgs
         for (int k = 0; k < 12; ++k)
           if (ox0 + k / 3 < Wo) a.out_u8[o + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// encode_0 -> encode_1 fused through LDS.  A workgroup owns TH1 rows x 16 columns of the
+// layer-1 output; it stages the (4 TH1 + 3) x 67 RGB pixels that feed them (normalised,
+// planar, columns split by col % 4), computes layer 0 (K = 27 -> 7 MFMA k-steps) on the
+// (2 TH1 + 1) x 33 layer-0 pixels layer 1 reads — written straight into layer 1's
+// column-deinterleaved LDS tile, zero outside the layer-0 image (layer 1's SAME pad) —
+// then runs layer 1 (stride-2 implicit GEMM, weights from L2 with register prefetch).
+// The full-resolution C0-channel layer-0 activation never reaches HBM.
+// ---------------------------------------------------------------------------------------
+template <int C0, int C1, int TH1, bool U8>
+__global__ void __launch_bounds__(256) enc01_kernel(const Enc01Args a) {
+  static_assert(C0 % 16 == 0 && C1 % 16 == 0 && (TH1 % 4 == 0 || TH1 == 2), "tile");
+  constexpr int R0 = 4 * TH1 + 3;        // RGB rows
+  constexpr int QJ = 17;                 // entries per col%4 plane (67 cols -> 17)
+  constexpr int RGBP = R0 * 4 * QJ;      // floats per channel plane
+  constexpr int LR1 = 2 * TH1 + 1, LC1 = 34, PS1 = C0 + 8;
+  constexpr int T1 = LR1 * LC1 * PS1;    // layer-1 input tile (floats)
+  constexpr int NSLOT = LR1 * LC1;
+  constexpr int NBLK0 = (NSLOT + 15) / 16;
+  constexpr int NB0 = C0 / 16;
+  constexpr int KC1 = C0 / 16;
+  constexpr int WR = TH1 >= 4 ? 4 : 2;   // waves split rows x channel blocks for layer 1
+  constexpr int WC = 4 / WR;
+  constexpr int MB = TH1 / WR;
+  constexpr int NB1 = C1 / 16 / WC;
+  static_assert((C1 / 16) % WC == 0, "layer-1 channel split");
+  __shared__ __attribute__((aligned(16))) float smem[T1 + 3 * RGBP];
+  float* const t1 = smem;
+  float* const rgb = smem + T1;
+
+  const int tid = threadIdx.x;
+  const int gx0 = blockIdx.x * 16, gy0 = blockIdx.y * TH1, nimg = blockIdx.z;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
+
+  // layer-1 weight prefetch starts before anything else
+  constexpr int PF = 2, NSTEP = 9 * KC1;
+  const int wr = wave / WC, wc = wave % WC;
+  const int co_wave = wc * NB1 * 16;
+  const float* __restrict__ wl = a.wp1 + (size_t)(lg * C1 + co_wave + li) * 4;
+  auto wglob = [&](int s, int nb) -> f32x4 {
+    const int tap = s / KC1, kc = s % KC1;
+    return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC1 + kc) * 4 * C1 * 4 + nb * 64);
+  };
+  f32x4 av[PF + 1][NB1];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int nb = 0; nb < NB1; ++nb) av[p][nb] = wglob(p, nb);
+
+  // ---- stage normalised RGB: rows 2*(2 gy0 - pad1y) - pad0y + rr, cols likewise ----
+  const int ey0 = 2 * gy0 - a.pad1y, ex0 = 2 * gx0 - a.pad1x;   // first layer-0 pixel
+  const int iy0 = 2 * ey0 - a.pad0y, ix0 = 2 * ex0 - a.pad0x;   // first RGB pixel
+  auto put_rgb = [&](int rr, int col, int c, float x) {
+    rgb[c * RGBP + (rr * 4 + (col & 3)) * QJ + (col >> 2)] = __fdiv_rn(__fsub_rn(x, a.mean[c]), a.std[c]);
+  };
+  // zero the planes first where the tile leaves the image (SAME padding)
+  const bool edge = iy0 < 0 || ix0 < 0 || iy0 + R0 > a.H || ix0 + 67 > a.W || !U8 || (ix0 * 3) % 4 != 0;
+  if (edge) {
+    for (int e = tid; e < 3 * RGBP; e += 256) rgb[e] = 0.f;
+    __syncthreads();
+  }
+  if constexpr (U8) {
+    if (!edge) {
+      // interior: each thread unpacks 32-bit words of the 201-byte RGB row segments
+      constexpr int WPR = 51;  // 204 bytes >= 67 * 3
+      for (int e = tid; e < R0 * WPR; e += 256) {
+        const int rr = e / WPR, w = e % WPR;
+        const size_t boff = ((size_t)(nimg * a.H + iy0 + rr) * a.W + ix0) * 3 + 4 * w;
+        const uint32_t word = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + boff);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pb = 4 * w + i;
+          if (pb < 201) put_rgb(rr, pb / 3, pb % 3, (float)((word >> (8 * i)) & 0xff));
+        }
+      }
+    }
+  }
+  if (edge) {
+    for (int e = tid; e < R0 * 67; e += 256) {
+      const int rr = e / 67, col = e % 67;
+      const int iy = iy0 + rr, ix = ix0 + col;
+      if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+        const size_t off = ((size_t)(nimg * a.H + iy) * a.W + ix) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float x;
+          if constexpr (U8) x = reinterpret_cast<const uint8_t*>(a.in)[off + c];
+          else x = reinterpret_cast<const float*>(a.in)[off + c];
+          put_rgb(rr, col, c, x);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- layer 0 on every slot of the layer-1 input tile ----
+  {
+    f32x4 w0[NB0], w1[NB0], bb[NB0];
+#pragma unroll
+    for (int nb = 0; nb < NB0; ++nb) {
+      const float* wq = a.wp0 + ((nb * 16 + li) * 4 + lg) * 8;
+      w0[nb] = *reinterpret_cast<const f32x4*>(wq);
+      w1[nb] = *reinterpret_cast<const f32x4*>(wq + 4);
+      bb[nb] = *reinterpret_cast<const f32x4*>(a.b0 + nb * 16 + lg * 4);
+    }
+    // per-lane LDS offsets of the 7 k-steps (k = 4t + lg -> channel, ky, kx), per column
+    // plane of the slot: offset = c*RGBP + ky*4*QJ + ((2 plane + kx) & 3)*QJ + ((2 plane + kx) >> 2)
+    int dl[2][7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      const int k = 4 * t + lg;
+      const int tap = k / 3, c = k - 3 * (k / 3);
+      const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) {
+        const int q = 2 * pl + kx;
+        dl[pl][t] = k < 27 ? c * RGBP + ky * 4 * QJ + (q & 3) * QJ + (q >> 2) : -1;
+      }
+    }
+    for (int blk = wave; blk < NBLK0; blk += 4) {
+      const int slot = blk * 16 + li;
+      const int r = slot / LC1, cs = slot % LC1;
+      const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
+      const int exl = 2 * j + plane;  // layer-0 column (local)
+      const int base = 2 * r * 4 * QJ + j;
+      const bool rd = slot < NSLOT && exl < 33;
+      float b[7];
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        const int d = plane ? dl[1][t] : dl[0][t];
+        b[t] = (rd && d >= 0) ? rgb[base + d] : 0.f;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[NB0];
+#pragma unroll
+      for (int nb = 0; nb < NB0; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 7; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NB0; ++nb) acc[nb] = mfma4(t < 4 ? w0[nb][t & 3] : w1[nb][t & 3], b[t], acc[nb]);
+      // lane holds channels nb*16 + 4 lg .. +3 of slot; relu; zero outside layer 0's image
+      const int ey = ey0 + r, ex = ex0 + exl;
+      const bool valid = rd && ey >= 0 && ey < a.H1 && ex >= 0 && ex < a.W1;
+      if (slot < NSLOT) {
+#pragma unroll
+        for (int nb = 0; nb < NB0; ++nb) {
+          f32x4 v = acc[nb];
+          v.x = valid ? fmaxf(__fadd_rn(v.x, bb[nb].x), 0.f) : 0.f;
+          v.y = valid ? fmaxf(__fadd_rn(v.y, bb[nb].y), 0.f) : 0.f;
+          v.z = valid ? fmaxf(__fadd_rn(v.z, bb[nb].z), 0.f) : 0.f;
+          v.w = valid ? fmaxf(__fadd_rn(v.w, bb[nb].w), 0.f) : 0.f;
+          *reinterpret_cast<f32x4*>(&t1[slot * PS1 + nb * 16 + lg * 4]) = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- layer 1: stride-2 implicit GEMM from the LDS tile ----
+  f32x4 acc[MB][NB1];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB1; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto load_b = [&](int s, f32x4* dst) {
+    const int tap = s / KC1, kc = s % KC1, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int r = wr * MB + mb;
+      const int lp = (2 * r + ky) * LC1 + (kx & 1) * 17 + li + (kx >> 1);
+      dst[mb] = *reinterpret_cast<const f32x4*>(&t1[lp * PS1 + kc * 16 + lg * 4]);
+    }
+  };
+  f32x4 bq[2][MB];
+  load_b(0, bq[0]);
+#pragma unroll
+  for (int s = 0; s < NSTEP; ++s) {
+    const int c = s & 1;
+    if (s + PF < NSTEP) {
+#pragma unroll
+      for (int nb = 0; nb < NB1; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
+    }
+    if (s + 1 < NSTEP) load_b(s + 1, bq[c ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB1; ++nb) acc[mb][nb] = mfma4(av[s % (PF + 1)][nb][t], bq[c][mb][t], acc[mb][nb]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int oy = gy0 + wr * MB + mb, ox = gx0 + li;
+    if (oy >= a.H2 || ox >= a.W2) continue;
+#pragma unroll
+    for (int nb = 0; nb < NB1; ++nb) {
+      const int co = co_wave + nb * 16 + lg * 4;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
+      f32x4 v = acc[mb][nb];
+      v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
+      v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
+      v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
+      v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
+      *reinterpret_cast<f32x4*>(a.out + ((size_t)(nimg * a.H2 + oy) * a.W2 + ox) * C1 + co) = v;
     }
   }
 }

@@ -36,6 +36,32 @@ bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream
 // Variants 0-2: dense sub-pixel form, TH 4/8/16 (one summation order: autotuned).
 // Variants 3-5: scatter form, TH 4/8/16 (different tap summation order; chosen only via
 // TIC_RGB_OUT_FORM=scatter so that tuning never changes results).
+int enc01_variants() { return 2; }  // TH1 = 2, 4
+
+template <int C0, int C1, int TH1>
+static bool enc01_th(bool u8_input, const Enc01Args& a, int n, hipStream_t s) {
+  dim3 grid((a.W2 + 15) / 16, (a.H2 + TH1 - 1) / TH1, n);
+  if (u8_input)
+    hipLaunchKernelGGL((enc01_kernel<C0, C1, TH1, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((enc01_kernel<C0, C1, TH1, false>), grid, dim3(256), 0, s, a);
+  return true;
+}
+
+template <int C0, int C1>
+static bool enc01_c(bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant) {
+  if (variant == 0) return enc01_th<C0, C1, 2>(u8_input, a, n, s);
+  if (variant == 1) return enc01_th<C0, C1, 4>(u8_input, a, n, s);
+  return false;
+}
+
+bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant) {
+  if (c0 == 32 && c1 == 32) return enc01_c<32, 32>(u8_input, a, n, s, variant);
+  if (c0 == 16 && c1 == 32) return enc01_c<16, 32>(u8_input, a, n, s, variant);
+  if (c0 == 32 && c1 == 64) return enc01_c<32, 64>(u8_input, a, n, s, variant);
+  return false;
+}
+
 int rgb_out_variants() { return 3; }
 
 template <int CIN, int TH, bool SCATTER>

@@ -25,6 +25,7 @@ struct ConvArgs {
   int Ho, Wo;          // output spatial
   int pad_y, pad_x;    // SAME pad_before (S1: 1; S2: 0 for even input, 1 for odd; T2: unused)
   float qscale;        // Q - 1
+  int num_cus;         // compute units (persistent variants size their grid from it)
 };
 
 struct RgbInArgs {
@@ -34,6 +35,21 @@ struct RgbInArgs {
   float* out;          // [N,Ho,Wo,Cout]
   int H, W, Ho, Wo;
   int pad_y, pad_x;    // SAME pad_before of the stride-2 conv
+  float mean[3], std[3];
+};
+
+// First two analysis layers fused through LDS (RGB -> C0 stride 2 -> C1 stride 2).
+struct Enc01Args {
+  const void* in;      // [N,H,W,3] u8 or f32 RGB
+  const float* wp0;    // layer 0, RGB packing [C0][4][8]
+  const float* b0;     // [C0]
+  const float* wp1;    // layer 1, generic packing [tap][C0/16][4][C1][4]
+  const float* b1;     // [C1]
+  float* out;          // [N,H2,W2,C1]
+  int H, W;            // RGB size
+  int H1, W1;          // layer-0 output size
+  int H2, W2;          // layer-1 output size
+  int pad0y, pad0x, pad1y, pad1x;  // SAME pad_before of both convs
   float mean[3], std[3];
 };
 
@@ -54,7 +70,8 @@ struct ConvEntry {
   int mode, cin, cout, act, res, in, out;
   int th;             // output rows per block (input rows for T2)
   int nsplit;         // workgroups splitting the output channels of one pixel tile
-  int wlds;           // weights staged through LDS by LDS-DMA (1) or read from L2 (0)
+  int wlds;           // weights staged through LDS by LDS-DMA (1) or read from L2 (0);
+                      // 2: persistent loader/consumer variant (conv3x3_pipe_kernel)
   ConvLaunch fn;
 };
 
@@ -66,6 +83,8 @@ const ConvEntry* conv_registry_t2(int* count);
 // First / last layer launchers (conv_rgb.hip); `variant` < rgb_*_variants() selects the
 // tiling / formulation; return false if the width is not compiled.
 int rgb_in_variants();
+int enc01_variants();
+bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant);
 int rgb_out_variants();
 bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant);
 bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant);

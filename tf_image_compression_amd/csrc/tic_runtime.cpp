@@ -15,6 +15,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -261,9 +262,21 @@ struct LayerRT {
   std::map<int, int> tuned_var;                 // first/last layer: batch size -> variant
 };
 
+// An execution lane: a HIP stream and its own activation workspace.  Lane 0's stream is
+// the handle's stream; with 2 lanes a batch is split in halves that run concurrently so
+// one half's launch ramp / staging / tail overlaps the other half's MFMA work.
+struct Lane {
+  hipStream_t stream = nullptr;
+  float* ws[3] = {nullptr, nullptr, nullptr};
+  int ws_batch = 0;
+};
+
 struct tic_handle {
   int model_id = 0, P = 0, Q = 2, device = 0;
   hipStream_t stream = nullptr;
+  Lane lanes[2];
+  int nlanes = 2;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<LayerRT> layers;
   int n_enc = 0;
   float mean[3] = {0, 0, 0}, std[3] = {1, 1, 1};
@@ -271,8 +284,6 @@ struct tic_handle {
   float* d_lut = nullptr;
   int chunk = 256;
   size_t act_elems = 0;  // max f32 activation elements per patch
-  int ws_batch = 0;
-  float* ws[3] = {nullptr, nullptr, nullptr};
   // host-entry staging
   void* st_in = nullptr;
   size_t st_in_bytes = 0;
@@ -282,6 +293,17 @@ struct tic_handle {
   size_t st_out2_bytes = 0;
   std::vector<void*> user_allocs;
   int tune_reps = 0;  // > 0 while tic_autotune runs
+  int num_cus = 256;
+  bool use_graph = false;
+  bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); measured slower, opt-in
+  struct GraphKey {
+    const void *in, *idx, *rgb;
+    int n, nlanes;
+    bool operator<(const GraphKey& o) const {
+      return std::tie(in, idx, rgb, n, nlanes) < std::tie(o.in, o.idx, o.rgb, o.n, o.nlanes);
+    }
+  };
+  std::map<GraphKey, hipGraphExec_t> graphs;  // captured encode->decode sequences
   bool rmbe() const { return model_id == TIC_MODEL_RMBE; }
 };
 
@@ -297,16 +319,21 @@ int ensure(void** p, size_t* have, size_t need) {
   return TIC_OK;
 }
 
-int ensure_ws(tic_handle* h, int n) {
-  if (h->ws_batch >= n) return TIC_OK;
-  for (auto& b : h->ws) {
+int ensure_ws(tic_handle* h, Lane& ln, int n) {
+  if (ln.ws_batch >= n) return TIC_OK;
+  for (auto& b : ln.ws) {
     if (b) (void)hipFree(b);
     b = nullptr;
   }
-  h->ws_batch = 0;
-  for (auto& b : h->ws) HIP_TRY(hipMalloc((void**)&b, h->act_elems * (size_t)n * sizeof(float)));
-  h->ws_batch = n;
+  ln.ws_batch = 0;
+  for (auto& b : ln.ws) HIP_TRY(hipMalloc((void**)&b, h->act_elems * (size_t)n * sizeof(float)));
+  ln.ws_batch = n;
   return TIC_OK;
+}
+
+void clear_graphs(tic_handle* h) {
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
 }
 
 int check_launch() {
@@ -357,8 +384,10 @@ struct Prof {
 
 // Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
 // outputs per-position flags.  Buffers rotate through h->ws.
-int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_idx, float* d_pre,
+int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, uint8_t* d_idx, float* d_pre,
                uint8_t* d_rgb, float* d_f32, const Prof& prof) {
+  hipStream_t const st = ln.stream;
+  float* const* ws = ln.ws;
   const int L = (int)h->layers.size();
   int cur = -1;       // ws index holding the current activation (-1: external input)
   int block_in = -1;  // ws index of the enclosing res_block's input
@@ -378,14 +407,57 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
       }
     const bool starts_block = d.kind == K_S1 && !d.residual && li + 1 < L && h->layers[li + 1].def.residual;
     if (starts_block) block_in = cur;
-    const float* src = cur >= 0 ? h->ws[cur] : nullptr;
-    if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li], h->stream));
+    const float* src = cur >= 0 ? ws[cur] : nullptr;
+    if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li], st));
+    const bool fuse = first && h->fuse01 && li + 1 < l1 && h->layers[1].def.kind == K_S2 &&
+                      h->layers[1].def.act == 1 && !h->layers[1].def.residual &&
+                      !(!h->rmbe() && h->n_enc == 2);
+    if (fuse) {
+      LayerRT& l1r = h->layers[1];
+      tic::Enc01Args a{};
+      a.in = in;
+      a.wp0 = lay.d_w;
+      a.b0 = lay.d_b;
+      a.wp1 = l1r.d_w;
+      a.b1 = l1r.d_b;
+      a.out = ws[dst];
+      a.H = a.W = lay.h_in;
+      a.H1 = a.W1 = lay.h_out;
+      a.H2 = a.W2 = l1r.h_out;
+      a.pad0y = a.pad0x = same_pad(d.kind, lay.h_in);
+      a.pad1y = a.pad1x = same_pad(K_S2, l1r.h_in);
+      for (int c = 0; c < 3; ++c) {
+        a.mean[c] = h->mean[c];
+        a.std[c] = h->std[c];
+      }
+      auto it = lay.tuned_var.find(-n);  // fused-pair variants keyed by -n
+      int var = it != lay.tuned_var.end() ? it->second : 1;
+      if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
+        int rc = time_variants(st, tic::enc01_variants(), h->tune_reps,
+                               [&](int v) { return tic::launch_enc01(d.cout, l1r.def.cout, !h->rmbe(), a, n, st, v); },
+                               &var);
+        if (rc) return rc;
+        lay.tuned_var[-n] = var;
+      }
+      if (!tic::launch_enc01(d.cout, l1r.def.cout, !h->rmbe(), a, n, st, var))
+        return fail(TIC_EUNSUPPORTED, "fused first layers %d->%d->%d not compiled", d.cin, d.cout, l1r.def.cout);
+      int rc = check_launch();
+      if (rc) return rc;
+      if (prof.ev) {
+        HIP_TRY(hipEventRecord(prof.ev[1], st));
+        HIP_TRY(hipEventRecord(prof.ev[2], st));  // layer 1 ran inside layer 0's launch
+        HIP_TRY(hipEventRecord(prof.ev[3], st));
+      }
+      cur = dst;
+      ++li;  // layer 1 consumed
+      continue;
+    }
     if (first) {
       tic::RgbInArgs a{};
       a.in = in;
       a.wp = lay.d_w;
       a.bias = lay.d_b;
-      a.out = h->ws[dst];
+      a.out = ws[dst];
       a.H = a.W = lay.h_in;
       a.Ho = a.Wo = lay.h_out;
       a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
@@ -396,12 +468,12 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
       auto it = lay.tuned_var.find(n);
       int var = it != lay.tuned_var.end() ? it->second : kRgbInDefault;
       if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
-        int rc = time_variants(h->stream, tic::rgb_in_variants(), h->tune_reps,
-                               [&](int v) { return tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, h->stream, v); }, &var);
+        int rc = time_variants(st, tic::rgb_in_variants(), h->tune_reps,
+                               [&](int v) { return tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, st, v); }, &var);
         if (rc) return rc;
         lay.tuned_var[n] = var;
       }
-      if (!tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, h->stream, var))
+      if (!tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, st, var))
         return fail(TIC_EUNSUPPORTED, "first layer %s: width %d not compiled", d.name.c_str(), d.cout);
     } else if (last) {
       tic::RgbOutArgs a{};
@@ -421,12 +493,12 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
       const int forced = rgb_out_forced();
       if (forced >= 0) var = forced;
       else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
-        int rc = time_variants(h->stream, tic::rgb_out_variants(), h->tune_reps,
-                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, h->stream, v); }, &var);
+        int rc = time_variants(st, tic::rgb_out_variants(), h->tune_reps,
+                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, st, v); }, &var);
         if (rc) return rc;
         lay.tuned_var[n] = var;
       }
-      if (!tic::launch_rgb_out(d.cin, a, n, h->stream, var))
+      if (!tic::launch_rgb_out(d.cin, a, n, st, var))
         return fail(TIC_EUNSUPPORTED, "last layer %s: width %d not compiled", d.name.c_str(), d.cin);
     } else {
       const int inm = first_dec ? tic::IN_IDX : tic::IN_F32;
@@ -443,14 +515,15 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
       a.in = first_dec ? in : (const void*)src;
       a.wp = lay.d_w;
       a.bias = lay.d_b;
-      a.res = d.residual ? h->ws[block_in] : nullptr;
-      a.out = last_enc ? d_pre : h->ws[dst];
+      a.res = d.residual ? ws[block_in] : nullptr;
+      a.out = last_enc ? d_pre : ws[dst];
       a.qout = last_enc ? d_idx : nullptr;
       a.lut = h->d_lut;
       a.H = a.W = lay.h_in;
       a.Ho = a.Wo = lay.h_out;
       a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
       a.qscale = (float)(h->Q - 1);
+      a.num_cus = h->num_cus;
       if (h->tune_reps > 0 && it == lay.tuned.end()) {
         // time every compiled tiling on the live buffers (re-launching is idempotent)
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
@@ -458,14 +531,18 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
         HIP_TRY(hipEventCreate(&t0));
         HIP_TRY(hipEventCreate(&t1));
         float best_ms = 1e30f;
+        const bool log = getenv("TIC_TUNE_LOG") != nullptr;
         for (const tic::ConvEntry* c : cands) {
-          c->fn(a, n, h->stream);  // warm
-          HIP_TRY(hipEventRecord(t0, h->stream));
-          for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, h->stream);
-          HIP_TRY(hipEventRecord(t1, h->stream));
+          c->fn(a, n, st);  // warm
+          HIP_TRY(hipEventRecord(t0, st));
+          for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, st);
+          HIP_TRY(hipEventRecord(t1, st));
           HIP_TRY(hipEventSynchronize(t1));
           float ms = 0.f;
           HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+          if (log)
+            fprintf(stderr, "tune %-22s n=%d th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), n, c->th, c->nsplit,
+                    c->wlds, 1e3f * ms / h->tune_reps);
           if (ms < best_ms) {
             best_ms = ms;
             e = c;
@@ -477,11 +554,11 @@ int run_layers(tic_handle* h, int l0, int l1, const void* in, int n, uint8_t* d_
         if (rc) return rc;
         lay.tuned[n] = e;
       }
-      e->fn(a, n, h->stream);
+      e->fn(a, n, st);
     }
     int rc = check_launch();
     if (rc) return rc;
-    if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li + 1], h->stream));
+    if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li + 1], st));
     if (d.residual) block_in = -1;
     cur = dst;
   }
@@ -500,15 +577,38 @@ size_t code_elems(const tic_handle* h) {
   return (size_t)l.h_out * l.h_out * l.def.cout;
 }
 
-// chunked drivers (device pointers)
+// chunked drivers (device pointers).  Each chunk runs on lane 0, or is split in halves
+// over both lanes (fork/join with events on the handle's stream) when nlanes == 2.
+template <typename F>
+int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
+  if (h->nlanes < 2 || !allow_split || m < 2) {
+    int rc = ensure_ws(h, h->lanes[0], m);
+    if (rc) return rc;
+    return body(h->lanes[0], 0, m);
+  }
+  const int m0 = (m + 1) / 2, m1 = m - m0;
+  int rc = ensure_ws(h, h->lanes[0], m0);
+  if (!rc) rc = ensure_ws(h, h->lanes[1], m1);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+  HIP_TRY(hipStreamWaitEvent(h->lanes[1].stream, h->ev_fork, 0));
+  rc = body(h->lanes[0], 0, m0);
+  if (!rc) rc = body(h->lanes[1], m0, m1);
+  HIP_TRY(hipEventRecord(h->ev_join, h->lanes[1].stream));
+  HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  return rc;
+}
+
 int encode_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, float* pre, const Prof& prof) {
   const size_t in_pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
+  const bool split = !prof.ev && h->tune_reps == 0;
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = ensure_ws(h, m);
-    if (rc) return rc;
-    rc = run_layers(h, 0, h->n_enc, in + s * in_pp, m, idx + s * ce, pre ? pre + s * ce : nullptr, nullptr,
-                    nullptr, prof);
+    int rc = run_chunk(h, m, split, [&](Lane& ln, int o, int k) {
+      const int b = s + o;
+      return run_layers(h, ln, 0, h->n_enc, in + b * in_pp, k, idx + b * ce, pre ? pre + b * ce : nullptr,
+                        nullptr, nullptr, prof);
+    });
     if (rc) return rc;
   }
   return TIC_OK;
@@ -516,12 +616,31 @@ int encode_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, float* pre
 
 int decode_dev(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb, float* f32, const Prof& prof) {
   const size_t out_pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
+  const bool split = !prof.ev && h->tune_reps == 0;
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = ensure_ws(h, m);
+    int rc = run_chunk(h, m, split, [&](Lane& ln, int o, int k) {
+      const int b = s + o;
+      return run_layers(h, ln, h->n_enc, (int)h->layers.size(), idx + b * ce, k, nullptr, nullptr,
+                        rgb ? rgb + b * out_pp : nullptr, f32 ? f32 + b * out_pp : nullptr, prof);
+    });
     if (rc) return rc;
-    rc = run_layers(h, h->n_enc, (int)h->layers.size(), idx + s * ce, m, nullptr, nullptr,
-                    rgb ? rgb + s * out_pp : nullptr, f32 ? f32 + s * out_pp : nullptr, prof);
+  }
+  return TIC_OK;
+}
+
+// encode -> decode of one chunk back to back on each lane (no join in between)
+int codec_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, uint8_t* rgb) {
+  const size_t pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
+  for (int s = 0; s < n; s += h->chunk) {
+    const int m = std::min(h->chunk, n - s);
+    int rc = run_chunk(h, m, h->tune_reps == 0, [&](Lane& ln, int o, int k) {
+      const int b = s + o;
+      int r = run_layers(h, ln, 0, h->n_enc, in + b * pp, k, idx + b * ce, nullptr, nullptr, nullptr, Prof{nullptr});
+      if (r) return r;
+      return run_layers(h, ln, h->n_enc, (int)h->layers.size(), idx + b * ce, k, nullptr, nullptr, rgb + b * pp,
+                        nullptr, Prof{nullptr});
+    });
     if (rc) return rc;
   }
   return TIC_OK;
@@ -529,11 +648,14 @@ int decode_dev(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb, float* f3
 
 int rmbe_dev(tic_handle* h, const float* in, int n, float* out, const Prof& prof) {
   const size_t pp = (size_t)h->P * h->P * 3;
+  const bool split = !prof.ev && h->tune_reps == 0;
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = ensure_ws(h, m);
-    if (rc) return rc;
-    rc = run_layers(h, 0, (int)h->layers.size(), in + s * pp, m, nullptr, nullptr, nullptr, out + s * pp, prof);
+    int rc = run_chunk(h, m, split, [&](Lane& ln, int o, int k) {
+      const int b = s + o;
+      return run_layers(h, ln, 0, (int)h->layers.size(), in + b * pp, k, nullptr, nullptr, nullptr, out + b * pp,
+                        prof);
+    });
     if (rc) return rc;
   }
   return TIC_OK;
@@ -601,6 +723,11 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   h->P = patch_size;
   h->Q = quan_scale;
   h->device = device;
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      h->num_cus = prop.multiProcessorCount;
+  }
   int hh = patch_size;
   size_t act = 0;
   for (const LayerDef& d : table) {
@@ -615,11 +742,16 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   }
   h->act_elems = act;
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
+  if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(2, std::max(1, atoi(c)));
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->lanes[1].stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete h;
-    return fail(TIC_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    return fail(TIC_EHIP, "stream/event creation: %s", hipGetErrorString(e));
   }
+  h->lanes[0].stream = h->stream;
   *out = h;
   return TIC_OK;
 }
@@ -633,8 +765,16 @@ void tic_destroy(tic_handle* h) {
     if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_b) (void)hipFree(l.d_b);
   }
-  for (auto& b : h->ws)
-    if (b) (void)hipFree(b);
+  clear_graphs(h);
+  for (auto& ln : h->lanes)
+    for (auto& b : ln.ws)
+      if (b) (void)hipFree(b);
+  if (h->lanes[1].stream) {
+    (void)hipStreamSynchronize(h->lanes[1].stream);
+    (void)hipStreamDestroy(h->lanes[1].stream);
+  }
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->d_lut) (void)hipFree(h->d_lut);
   if (h->st_in) (void)hipFree(h->st_in);
   if (h->st_out) (void)hipFree(h->st_out);
@@ -695,6 +835,8 @@ int tic_finalize(tic_handle* h) {
     if (!l.has_b) return fail(TIC_ESTATE, "missing variable %s/bias", l.def.name.c_str());
   }
   HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  clear_graphs(h);
   const int L = (int)h->layers.size();
   for (int i = 0; i < L; ++i) {
     LayerRT& l = h->layers[i];
@@ -796,9 +938,64 @@ int tic_decode_device(tic_handle* h, const uint8_t* d_idx, int n, uint8_t* d_rgb
 }
 
 int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, uint8_t* d_rgb) {
-  int rc = tic_encode_device(h, d_patches, n, d_idx, nullptr);
+  int rc = check_ready(h);
   if (rc) return rc;
-  return tic_decode_device(h, d_idx, n, d_rgb, nullptr);
+  if (h->rmbe()) return fail(TIC_EINVAL, "rmbe handle: use tic_rmbe");
+  if (n < 0 || (n > 0 && (!d_patches || !d_idx || !d_rgb))) return fail(TIC_EINVAL, "bad arguments");
+  if (n == 0) return TIC_OK;
+  if (!h->use_graph) return codec_dev(h, d_patches, n, d_idx, d_rgb);
+  // HIP graph of the whole launch sequence (both lanes), captured on first use per
+  // (buffers, n); workspaces are allocated by an eager run before capture.
+  const tic_handle::GraphKey key{d_patches, d_idx, d_rgb, n, h->nlanes};
+  auto it = h->graphs.find(key);
+  if (it == h->graphs.end()) {
+    rc = codec_dev(h, d_patches, n, d_idx, d_rgb);  // eager: allocates, fills tuned choices
+    if (rc) return rc;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    rc = codec_dev(h, d_patches, n, d_idx, d_rgb);
+    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(TIC_EHIP, "graph capture: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(TIC_EHIP, "graph instantiate: %s", hipGetErrorString(e));
+    it = h->graphs.emplace(key, ge).first;
+    return TIC_OK;
+  }
+  HIP_TRY(hipGraphLaunch(it->second, h->stream));
+  return TIC_OK;
+}
+
+int tic_set_option(tic_handle* h, const char* key, int value) {
+  if (!h || !key) return fail(TIC_EINVAL, "null argument");
+  const std::string k(key);
+  if (k == "streams") {
+    if (value < 1 || value > 2) return fail(TIC_EINVAL, "streams must be 1 or 2");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->nlanes = value;
+    return TIC_OK;
+  }
+  if (k == "chunk") {
+    if (value < 1) return fail(TIC_EINVAL, "chunk must be >= 1");
+    h->chunk = value;
+    return TIC_OK;
+  }
+  if (k == "fuse01") {
+    clear_graphs(h);
+    h->fuse01 = value != 0;
+    return TIC_OK;
+  }
+  if (k == "graph") {
+    h->use_graph = value != 0;
+    return TIC_OK;
+  }
+  return fail(TIC_EINVAL, "unknown option %s", key);
 }
 
 int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out) {
@@ -926,7 +1123,9 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
   for (auto& l : h->layers) {
     l.tuned.erase(n);
     l.tuned_var.erase(n);
+    l.tuned_var.erase(-n);
   }
+  clear_graphs(h);
   void *d_idx = nullptr, *d_out = nullptr;
   const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
   const size_t px = (size_t)n * h->P * h->P * 3;
@@ -1012,6 +1211,7 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.Wo = out_size(kind, W);
   a.pad_y = same_pad(kind, H);
   a.pad_x = same_pad(kind, W);
+  a.num_cus = h->num_cus;
   e->fn(a, n, h->stream);
   int rc = check_launch();
   hipError_t se = hipStreamSynchronize(h->stream);

@@ -19,7 +19,7 @@ for k in ("parity", "cpu_baseline", "stats_allgather"):
 lp = os.path.join(ROOT, "gpurun_out", "bench_layers.json")
 if os.path.exists(lp):
     L = json.load(open(lp))
-    B = L["config"]["global_batch"] // max(1, d["n_gpus"])
+    B = L.get("lane_batch", L["config"]["global_batch"] // max(1, d["n_gpus"]))
     tot = 0
     for r in L["layers"]:
         tot += r["ms"]
