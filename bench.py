@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="execution lanes per GPU (1 or 2)")
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
+    ap.add_argument("--graph", action="store_true", help="replay the launch sequence as a HIP graph (opt-in)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                    help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic")
     ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
     return ap.parse_args()
 
@@ -147,7 +149,7 @@ def main():
     args = parse()
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
-    from tf_image_compression_amd.topology import bottleneck_shape
+    from tf_image_compression_amd.topology import bottleneck_shape, layer_table
     from tf_image_compression_amd import dist
 
     rank, world, local = dist.env_rank()
@@ -159,7 +161,7 @@ def main():
     params = synthetic_params(M, seed=0)
     codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local)
     codec.set_option("streams", args.streams)
-    codec.set_option("graph", 0 if args.no_graph else 1)
+    codec.set_option("graph", 1 if args.graph else 0)
     comm = dist.make_comm(codec)
     eh, ew, ec = bottleneck_shape(M, P)
 
@@ -203,17 +205,21 @@ def main():
     groups, rows = kernel_groups(codec, M, P, ms)
     dom_key = max(groups, key=lambda k: groups[k]["ms"])
     roof, dom_ms, dom_flops, dom_bytes = roofline_of(groups[dom_key], lane_b)
+    # HBM bytes per launch of the dominant kernel instance from the committed PMC summary
+    # (tools/pmc_box.sh + tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
+    kernels = codec.layer_kernels(lane_b)
+    names = {lay.name: i for i, lay in enumerate(layer_table(M))}
+    dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]})
     roof["traffic"] = None
-    traffic_file = os.path.join(ROOT, "profiles", "traffic_r01.json")
-    if os.path.exists(traffic_file):
-        try:
-            tr = json.load(open(traffic_file))
-            ent = tr.get(",".join(map(str, dom_key)))
-            if ent is not None:
-                roof["traffic"] = ent
-        except Exception:
-            pass
+    roof["traffic_source"] = None
+    if os.path.exists(args.traffic):
+        tr = json.load(open(args.traffic))
+        ents = [tr[k] for k in dom_kernels if k in tr]
+        if ents:
+            roof["traffic"] = round(float(np.mean([e["bytes"] for e in ents])))
+            roof["traffic_source"] = os.path.relpath(args.traffic, ROOT)
     roof["kernel"] = "+".join(groups[dom_key]["layers"])
+    roof["kernel_instance"] = dom_kernels
     roof["ms_per_launch"] = round(dom_ms, 5)
 
     step_ms = t_max * 1e3 / args.steps
@@ -237,15 +243,16 @@ def main():
                    "code_shape": [eh, ew, ec], "parallelism": f"image-parallel x{world}"},
         "roofline": roof,
         "roofline_step_frac": round(step_roofline(rows, B, step_ms), 4),
-        "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "hip_graph": not args.no_graph},
+        "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "hip_graph": bool(args.graph)},
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
                             "raw_bpp": round(summary["bpp"], 4)},
     }
     if rank == 0:
         try:
             os.makedirs(os.path.dirname(args.layers_out), exist_ok=True)
-            for r, v in zip(rows, codec.layer_variants(lane_b)):
+            for r, v, kn in zip(rows, codec.layer_variants(lane_b), kernels):
                 r["tile"] = list(v)
+                r["kernel"] = kn
             json.dump({"config": out["config"], "step_ms": step_ms, "lane_batch": lane_b, "layers": rows,
                        "groups": {",".join(map(str, k)): {"layers": g["layers"], "ms": g["ms"]}
                                   for k, g in groups.items()}},

@@ -128,6 +128,10 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps);
 /* Tiling used by layer i for batch n: rows per workgroup and channel split, the latter
  * + 100 when the weights are staged through LDS (0,0 if the layer has one fixed kernel). */
 int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit);
+/* Kernel instance layer i launches for batch n, as "<kernel>" "<template args>" in the
+ * form tools/pmc_summary.py prints (e.g. "conv3x3<1,32,32,4,4,1,false,1,false,0,0>");
+ * empty when the layer runs inside the previous layer's launch.  cap includes the NUL. */
+int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap);
 
 /* Unit-test entry: one layer on device float32 NHWC tensors.
  * kind/act as tic_layer_info; res (nullable) is added after the activation.

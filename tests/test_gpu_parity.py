@@ -37,7 +37,7 @@ def lib_codec():
         c.close()
 
 
-TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1)] for wl in (0, 1, 2)]
+TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1)] for wl in (0, 1)]
 
 LAYER_CASES = [
     (K_S1, 64, 64, 1, False, 16, 16),

@@ -192,6 +192,15 @@ class Codec:
             out.append((th.value, ns.value))
         return out
 
+    def layer_kernels(self, n: int):
+        """Kernel instance each layer launches for batch n ('' if fused into the previous)."""
+        out = []
+        for i in range(len(self.layers())):
+            buf = C.create_string_buffer(160)
+            check(lib().tic_layer_kernel(self._h, i, n, buf, 160), "tic_layer_kernel")
+            out.append(buf.value.decode())
+        return out
+
     def conv3x3_device(self, kind: int, act: int, d_in: DeviceBuffer, n: int, H: int, W: int, cin: int,
                        cout: int, kernel: np.ndarray, bias: np.ndarray, d_res: DeviceBuffer | None,
                        d_out: DeviceBuffer) -> None:

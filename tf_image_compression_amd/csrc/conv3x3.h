@@ -328,218 +328,6 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Persistent loader/consumer variant of conv3x3_kernel (same tiling, same tap-major fma
-// order -> bit-identical results).  320 threads: waves 0-3 compute exactly as above, wave 4
-// only moves data — it stages tile i+1's input (with halo) into the other half of a
-// double-buffered LDS tile while the compute waves run tile i.  vmcnt is per wave, so the
-// compute waves' weight-fragment waits never wait on the loader's global loads.  Each
-// workgroup walks tiles blockIdx.x, blockIdx.x + gridDim.x, ...  (grid = min(tiles,
-// CUs x resident workgroups)).
-// ---------------------------------------------------------------------------------------
-template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, int ACT, bool RES, int IN, int OUT>
-__global__ void __launch_bounds__(320) conv3x3_pipe_kernel(const ConvArgs a, int ntx, int nty, int ntiles) {
-  constexpr int PS = CIN + 8;
-  constexpr int KC = CIN / 16;
-  constexpr int COUT_WG = COUT / NSPLIT;
-  constexpr int NBT = COUT_WG / 16;
-  constexpr int WC = 4 / WR;
-  static_assert(WR * WC == 4 && TH % WR == 0 && NBT % WC == 0, "bad wave split");
-  constexpr int NB = NBT / WC;
-  constexpr int MB = TH / WR;
-  constexpr int NPH = MODE == MODE_T2 ? 4 : 1;
-  constexpr int LR = TileGeom<MODE, TH>::LR;
-  constexpr int LC = TileGeom<MODE, TH>::LC;
-  constexpr int C4 = CIN / 4;
-  constexpr int NSTEP = 9 * KC;
-  constexpr int TILE = LR * LC * PS;
-  constexpr int NSTAGE = LR * LC * C4;
-  __shared__ __attribute__((aligned(16))) float smem[2 * TILE];
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int H = a.H, W = a.W;
-
-  auto decode_tile = [&](int t, int& split, int& gx0, int& gy0, int& nimg) {
-    split = t % NSPLIT;
-    int r = t / NSPLIT;
-    gx0 = (r % ntx) * 16;
-    r /= ntx;
-    gy0 = (r % nty) * TH;
-    nimg = r / nty;
-  };
-  // loader wave: global -> registers (batches of 16 float4 per lane) -> LDS buffer
-  auto load_tile = [&](int t, float* dst) {
-    int split, gx0, gy0, nimg;
-    decode_tile(t, split, gx0, gy0, nimg);
-    constexpr int NIT = (NSTAGE + 63) / 64;
-    constexpr int SB = NIT < 16 ? NIT : 16;
-#pragma unroll
-    for (int i0 = 0; i0 < NIT; i0 += SB) {
-      f32x4 tmp[SB];
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        const int e = (i0 + i) * 64 + lane;
-        tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (i0 + i < NIT && e < NSTAGE) {
-          const int c4 = e % C4, pe = e / C4, col = pe % LC, row = pe / LC;
-          int iy, ix;
-          if constexpr (MODE == MODE_S2) {
-            const int plane = col >= 17 ? 1 : 0;
-            iy = 2 * gy0 + row - a.pad_y;
-            ix = 2 * gx0 + 2 * (col - plane * 17) + plane - a.pad_x;
-          } else if constexpr (MODE == MODE_S1) {
-            iy = gy0 - a.pad_y + row;
-            ix = gx0 - a.pad_x + col;
-          } else {
-            iy = gy0 - 1 + row;
-            ix = gx0 - 1 + col;
-          }
-          if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-            const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4;
-            if constexpr (IN == IN_F32) {
-              tmp[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
-            } else {
-              const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
-              tmp[i].x = a.lut[q & 0xff];
-              tmp[i].y = a.lut[(q >> 8) & 0xff];
-              tmp[i].z = a.lut[(q >> 16) & 0xff];
-              tmp[i].w = a.lut[q >> 24];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        const int e = (i0 + i) * 64 + lane;
-        if (i0 + i < NIT && e < NSTAGE) *reinterpret_cast<f32x4*>(&dst[(e / C4) * PS + (e % C4) * 4]) = tmp[i];
-      }
-    }
-  };
-
-  int t = blockIdx.x;
-  if (wave == 4 && t < ntiles) load_tile(t, smem);
-  __syncthreads();
-
-  const int wr = (wave & 3) / WC, wc = (wave & 3) % WC;
-  const int li = lane & 15, lg = lane >> 4;
-  const int co_wave = wc * NB * 16;
-  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
-    float* const lds = smem + (it & 1) * TILE;
-    if (wave == 4) {
-      if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x, smem + ((it + 1) & 1) * TILE);
-    } else {
-      int split, gx0, gy0, nimg;
-      decode_tile(t, split, gx0, gy0, nimg);
-      const int co_wg = split * COUT_WG;
-      const float* __restrict__ wl = a.wp + (size_t)(lg * COUT + co_wg + co_wave + li) * 4;
-      auto wglob = [&](int s, int nb) -> f32x4 {
-        const int tap = s / KC, kc = s % KC;
-        return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC + kc) * 4 * COUT * 4 + nb * 64);
-      };
-      constexpr int PF = 2;
-      f32x4 av[PF + 1][NB];
-#pragma unroll
-      for (int p = 0; p < PF; ++p)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) av[p][nb] = wglob(p, nb);
-      auto load_b = [&](int s, f32x4* dst) {
-        const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const int r = wr * MB + mb;
-          int lp;
-          if constexpr (MODE == MODE_S1) lp = (r + ky) * LC + li + kx;
-          else if constexpr (MODE == MODE_S2) lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
-          else lp = (r + 1 - (ky == 2)) * LC + li + 1 - (kx == 2);
-          dst[mb] = *reinterpret_cast<const f32x4*>(&lds[lp * PS + kc * 16 + lg * 4]);
-        }
-      };
-      f32x4 acc[NPH][MB][NB];
-#pragma unroll
-      for (int p = 0; p < NPH; ++p)
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 bq[2][MB];
-      load_b(0, bq[0]);
-#pragma unroll
-      for (int s = 0; s < NSTEP; ++s) {
-        const int tap = s / KC, ky = tap / 3, kx = tap % 3;
-        const int c = s & 1;
-        if (s + PF < NSTEP) {
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
-        }
-        if (s + 1 < NSTEP) load_b(s + 1, bq[c ^ 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        const int ph = MODE == MODE_T2 ? (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0) : 0;
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-          for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-              acc[ph][mb][nb] = mfma4(av[s % (PF + 1)][nb][tt], bq[c][mb][tt], acc[ph][mb][nb]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      const int Ho = a.Ho, Wo = a.Wo;
-#pragma unroll
-      for (int p = 0; p < NPH; ++p) {
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const int r = wr * MB + mb;
-          int oy, ox;
-          if constexpr (MODE == MODE_T2) {
-            if (gy0 + r >= H || gx0 + li >= W) continue;
-            oy = 2 * (gy0 + r) + (p >> 1);
-            ox = 2 * (gx0 + li) + (p & 1);
-          } else {
-            oy = gy0 + r;
-            ox = gx0 + li;
-            if (oy >= Ho || ox >= Wo) continue;
-          }
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) {
-            const int co = co_wg + co_wave + nb * 16 + lg * 4;
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + co);
-            f32x4 v = acc[p][mb][nb];
-            v.x = __fadd_rn(v.x, bb.x);
-            v.y = __fadd_rn(v.y, bb.y);
-            v.z = __fadd_rn(v.z, bb.z);
-            v.w = __fadd_rn(v.w, bb.w);
-            if constexpr (ACT == ACT_RELU) {
-              v.x = fmaxf(v.x, 0.f);
-              v.y = fmaxf(v.y, 0.f);
-              v.z = fmaxf(v.z, 0.f);
-              v.w = fmaxf(v.w, 0.f);
-            }
-            const size_t o = ((size_t)(nimg * Ho + oy) * Wo + ox) * COUT + co;
-            if constexpr (RES) {
-              const f32x4 rr = *reinterpret_cast<const f32x4*>(a.res + o);
-              v.x = __fadd_rn(v.x, rr.x);
-              v.y = __fadd_rn(v.y, rr.y);
-              v.z = __fadd_rn(v.z, rr.z);
-              v.w = __fadd_rn(v.w, rr.w);
-            }
-            if constexpr (OUT == OUT_F32) {
-              *reinterpret_cast<f32x4*>(a.out + o) = v;
-            } else {
-              if (a.out) *reinterpret_cast<f32x4*>(a.out + o) = v;
-              const uint32_t q = quant1(v.x, a.qscale) | (quant1(v.y, a.qscale) << 8) |
-                                 (quant1(v.z, a.qscale) << 16) | (quant1(v.w, a.qscale) << 24);
-              *reinterpret_cast<uint32_t*>(a.qout + o) = q;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------------------
 // First layer: stride-2 3x3 conv from 3-channel RGB (u8 or f32) with the normalisation
 // (x - mean) / std (model_0/model.py:44) fused into the LDS staging.  K = 27 (+1 zero)
 // = 7 MFMA k-steps; lane group g supplies k = 4t + g -> (tap, channel) = divmod(k, 3).

@@ -7,9 +7,7 @@
   TIC_CONV(MODE_S1, 64, 64, 4, 4, 1, ACT, RES, IN, OUT),               \
       TIC_CONV(MODE_S1, 64, 64, 4, 4, 2, ACT, RES, IN, OUT),           \
       TIC_CONV(MODE_S1, 64, 64, 8, 4, 1, ACT, RES, IN, OUT),           \
-      TIC_CONV(MODE_S1, 64, 64, 2, 2, 1, ACT, RES, IN, OUT),           \
-      TIC_PIPE(MODE_S1, 64, 64, 2, 2, 1, ACT, RES, IN, OUT),           \
-      TIC_PIPE(MODE_S1, 64, 64, 4, 4, 1, ACT, RES, IN, OUT)
+      TIC_CONV(MODE_S1, 64, 64, 2, 2, 1, ACT, RES, IN, OUT)
 
 namespace tic {
 static const ConvEntry kS1[] = {

@@ -18,19 +18,6 @@ static const ConvEntry kT2[] = {
     TIC_CONV(MODE_T2, 80, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 80, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 64, 64, 4, 4, 1, ACT_ID, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 32, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 32, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 32, 32, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 32, 32, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 32, 16, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 64, 2, 2, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_PIPE(MODE_T2, 80, 64, 2, 2, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_PIPE(MODE_T2, 80, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 64, 2, 2, 1, ACT_ID, false, IN_F32, OUT_F32),
-    TIC_PIPE(MODE_T2, 64, 64, 4, 4, 1, ACT_ID, false, IN_F32, OUT_F32),
 };
 const ConvEntry* conv_registry_t2(int* count) {
   *count = sizeof(kT2) / sizeof(kT2[0]);

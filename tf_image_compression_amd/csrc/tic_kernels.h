@@ -25,7 +25,6 @@ struct ConvArgs {
   int Ho, Wo;          // output spatial
   int pad_y, pad_x;    // SAME pad_before (S1: 1; S2: 0 for even input, 1 for odd; T2: unused)
   float qscale;        // Q - 1
-  int num_cus;         // compute units (persistent variants size their grid from it)
 };
 
 struct RgbInArgs {
@@ -69,9 +68,9 @@ typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);
 struct ConvEntry {
   int mode, cin, cout, act, res, in, out;
   int th;             // output rows per block (input rows for T2)
+  int wr;             // wave row-groups
   int nsplit;         // workgroups splitting the output channels of one pixel tile
   int wlds;           // weights staged through LDS by LDS-DMA (1) or read from L2 (0);
-                      // 2: persistent loader/consumer variant (conv3x3_pipe_kernel)
   ConvLaunch fn;
 };
 

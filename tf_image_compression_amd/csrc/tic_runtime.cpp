@@ -382,6 +382,12 @@ struct Prof {
   hipEvent_t* ev;  // 2 per layer, or nullptr
 };
 
+// encode_0 -> encode_1 through one enc01_kernel launch (opt-in "fuse01")
+static bool fuses01(const tic_handle* h) {
+  return h->fuse01 && h->layers.size() > 2 && h->layers[1].def.kind == K_S2 && h->layers[1].def.act == 1 &&
+         !h->layers[1].def.residual && !(!h->rmbe() && h->n_enc == 2);
+}
+
 // Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
 // outputs per-position flags.  Buffers rotate through h->ws.
 int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, uint8_t* d_idx, float* d_pre,
@@ -409,9 +415,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
     if (starts_block) block_in = cur;
     const float* src = cur >= 0 ? ws[cur] : nullptr;
     if (prof.ev) HIP_TRY(hipEventRecord(prof.ev[2 * li], st));
-    const bool fuse = first && h->fuse01 && li + 1 < l1 && h->layers[1].def.kind == K_S2 &&
-                      h->layers[1].def.act == 1 && !h->layers[1].def.residual &&
-                      !(!h->rmbe() && h->n_enc == 2);
+    const bool fuse = first && li + 1 < l1 && fuses01(h);
     if (fuse) {
       LayerRT& l1r = h->layers[1];
       tic::Enc01Args a{};
@@ -523,7 +527,6 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.Ho = a.Wo = lay.h_out;
       a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
       a.qscale = (float)(h->Q - 1);
-      a.num_cus = h->num_cus;
       if (h->tune_reps > 0 && it == lay.tuned.end()) {
         // time every compiled tiling on the live buffers (re-launching is idempotent)
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
@@ -1180,6 +1183,48 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
   return TIC_OK;
 }
 
+int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
+  if (!h || !name || cap <= 0) return fail(TIC_EINVAL, "null argument");
+  if (i < 0 || i >= (int)h->layers.size()) return fail(TIC_EINVAL, "layer index %d out of range", i);
+  const LayerRT& l = h->layers[i];
+  const LayerDef& d = l.def;
+  const int L = (int)h->layers.size();
+  const char* tf[2] = {"false", "true"};
+  char buf[160] = "";
+  if (fuses01(h) && (i == 0 || i == 1)) {
+    if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
+      auto iv = l.tuned_var.find(-n);
+      const int v = iv != l.tuned_var.end() ? iv->second : 1;
+      snprintf(buf, sizeof buf, "enc01_kernel<%d,%d,%d,%s>", d.cout, h->layers[1].def.cout, v == 0 ? 2 : 4,
+               tf[!h->rmbe()]);
+    }
+  } else if (i == 0 || i == L - 1) {
+    auto iv = l.tuned_var.find(n);
+    const int v = iv != l.tuned_var.end() ? iv->second : (i == 0 ? kRgbInDefault : kRgbOutDefault);
+    static const int th[3] = {4, 8, 16};
+    if (i == 0)
+      snprintf(buf, sizeof buf, "conv_rgb_s2_kernel<%d,%d,%s>", d.cout, th[v % 3], tf[!h->rmbe()]);
+    else
+      snprintf(buf, sizeof buf, "%s<%d,%d>", v >= 3 ? "convT_rgb_scatter_kernel" : "convT_rgb_kernel", d.cin,
+               th[v % 3]);
+  } else {
+    const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
+    const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
+    auto it = l.tuned.find(n);
+    const tic::ConvEntry* e =
+        it != l.tuned.end() ? it->second
+                            : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
+                                        last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n);
+    if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
+    snprintf(buf, sizeof buf, "conv3x3<%d,%d,%d,%d,%d,%d,%s,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th, e->wr,
+             e->nsplit, tf[e->wlds != 0], e->act, tf[e->res != 0], e->in, e->out);
+  }
+  const int len = (int)strlen(buf);
+  if (len + 1 > cap) return fail(TIC_EINVAL, "name buffer too small (%d < %d)", cap, len + 1);
+  memcpy(name, buf, len + 1);
+  return TIC_OK;
+}
+
 int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int n, int H, int W, int cin, int cout,
                        const float* w_host, const float* b_host, const float* d_res, float* d_out) {
   if (!h) return fail(TIC_EINVAL, "null handle");
@@ -1211,7 +1256,6 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.Wo = out_size(kind, W);
   a.pad_y = same_pad(kind, H);
   a.pad_x = same_pad(kind, W);
-  a.num_cus = h->num_cus;
   e->fn(a, n, h->stream);
   int rc = check_launch();
   hipError_t se = hipStreamSynchronize(h->stream);
