@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="execution lanes per GPU (1 or 2)")
+    ap.add_argument("--tune-step", type=int, default=1,
+                    help="rounds of in-situ (whole dual-lane step) tuning after the per-layer autotune; 0 = off")
     ap.add_argument("--graph", action="store_true", help="replay the launch sequence as a HIP graph (opt-in)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic")
@@ -175,6 +177,8 @@ def main():
     lane_b = (B + 1) // 2 if args.streams == 2 and B > 1 else B
     if not args.no_autotune:
         codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice, outside the timed region
+        if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
+            codec.autotune_step(d_in, B, rounds=args.tune_step, reps=5)
     for _ in range(args.warmup):
         codec.codec_device(d_in, B, d_idx, d_rgb)
     codec.synchronize()

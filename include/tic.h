@@ -103,7 +103,8 @@ int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out);
  * on two HIP streams that run concurrently — default 2, env TIC_STREAMS), "chunk" (max
  * patches per launch sequence, default 256, env TIC_MAX_CHUNK), "graph" (1: replay
  * tic_codec_device as a captured HIP graph per (buffers, n) — default 0: measured slower
- * than eager dual-lane launches on MI355X). */
+ * than eager dual-lane launches on MI355X), "persist_grid" (> 0: cap on the grid of the
+ * persistent conv variants, so that tests run several tiles per workgroup; default 0). */
 int tic_set_option(tic_handle* h, const char* key, int value);
 
 /* --- introspection / measurement --- */
@@ -125,6 +126,12 @@ int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float*
  * (or rmbe) pass over d_in[n] and keep the fastest per layer for batch size n (like
  * cuDNN's benchmark mode).  Untuned batch sizes use a grid-size heuristic. */
 int tic_autotune(tic_handle* h, const void* d_in, int n, int reps);
+/* In-situ tuning for tic_codec_device / tic_rmbe_device on n patches: each layer's
+ * variant is chosen by the time of the whole launch sequence as it runs (both lanes),
+ * greedy over the layers for `rounds` passes, each candidate timed as `reps` steps (min
+ * of 3).  Starts from tic_autotune's per-layer choice (run here if missing).  All
+ * candidates produce bit-identical results. */
+int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int reps);
 /* Tiling used by layer i for batch n: rows per workgroup and channel split, the latter
  * + 100 when the weights are staged through LDS (0,0 if the layer has one fixed kernel). */
 int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit);

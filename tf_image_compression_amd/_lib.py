@@ -52,6 +52,7 @@ SIGNATURES = [
     ("tic_profile_layers", C.c_int, [vp, vp, C.c_int, C.c_int, f32p]),
     ("tic_autotune", C.c_int, [vp, vp, C.c_int, C.c_int]),
     ("tic_layer_variant", C.c_int, [vp, C.c_int, C.c_int, i32p, i32p]),
+    ("tic_autotune_step", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int]),
     ("tic_layer_kernel", C.c_int, [vp, C.c_int, C.c_int, C.c_char_p, C.c_int]),
     ("tic_conv3x3_device", C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      f32p, f32p, vp, vp]),

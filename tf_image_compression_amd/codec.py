@@ -184,6 +184,10 @@ class Codec:
     def autotune(self, d_in: DeviceBuffer, n: int, reps: int = 5) -> None:
         check(lib().tic_autotune(self._h, d_in.ptr, n, reps), "tic_autotune")
 
+    def autotune_step(self, d_in: DeviceBuffer, n: int, rounds: int = 1, reps: int = 5) -> None:
+        """Per-layer variants chosen by the whole dual-lane step time (tic_autotune_step)."""
+        check(lib().tic_autotune_step(self._h, d_in.ptr, n, rounds, reps), "tic_autotune_step")
+
     def layer_variants(self, n: int):
         out = []
         for i in range(len(self.layers())):

@@ -64,12 +64,15 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // one 16-channel chunk of one 3x3 tap), so every tiling accumulates each output in the
 // same fma order (results are bit-identical across tilings).  Weights are packed
 // [tap][Cin/16][4 g][Cout][4 t]; their A fragments come either
-//   WLDS=false: straight from L2 into registers, prefetched PF steps ahead, or
-//   WLDS=true : from a 2-slot LDS ring holding one tap's slab for this workgroup's
-//               channels, filled by LDS-DMA (global_load_lds_dwordx4) one tap ahead and
-//               shared by the 4 waves (one barrier per tap).
-template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, bool WLDS, int ACT, bool RES, int IN, int OUT>
+//   WSRC=0: straight from L2 into registers, prefetched PF = 2 steps ahead,
+//   WSRC=2: the same with PF = 6 (small grids run ~1 wave per SIMD, so the prefetch
+//           alone has to cover the L2 latency), or
+//   WSRC=1: from a 2-slot LDS ring holding one tap's slab for this workgroup's
+//           channels, filled by LDS-DMA (global_load_lds_dwordx4) one tap ahead and
+//           shared by the 4 waves (one barrier per tap).
+template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, int WSRC, int ACT, bool RES, int IN, int OUT>
 __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
+  constexpr bool WLDS = WSRC == 1;
   static_assert(CIN % 16 == 0 && COUT % 16 == 0, "channels must be multiples of 16");
   constexpr int PS = CIN + 8;
   constexpr int KC = CIN / 16;
@@ -128,7 +131,7 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
     return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC + kc) * 4 * COUT * 4 + nb * 64);
   };
 
-  constexpr int PF = 2;  // register prefetch distance (WLDS=false)
+  constexpr int PF = WSRC == 2 ? 6 : 2;  // register prefetch distance (L2 sources)
   f32x4 av[WLDS ? 1 : PF + 1][NB];
   if constexpr (WLDS) {
     wdma(0, 0);

@@ -5,9 +5,12 @@
 
 #define S1_VARIANTS(ACT, RES, IN, OUT)                                 \
   TIC_CONV(MODE_S1, 64, 64, 4, 4, 1, ACT, RES, IN, OUT),               \
-      TIC_CONV(MODE_S1, 64, 64, 4, 4, 2, ACT, RES, IN, OUT),           \
+      TIC_CONV3(MODE_S1, 64, 64, 4, 4, 2, ACT, RES, IN, OUT),          \
       TIC_CONV(MODE_S1, 64, 64, 8, 4, 1, ACT, RES, IN, OUT),           \
-      TIC_CONV(MODE_S1, 64, 64, 2, 2, 1, ACT, RES, IN, OUT)
+      TIC_CONV3(MODE_S1, 64, 64, 2, 2, 1, ACT, RES, IN, OUT),          \
+      TIC_CONV3(MODE_S1, 64, 64, 2, 2, 2, ACT, RES, IN, OUT),          \
+      TIC_CONV3(MODE_S1, 64, 64, 4, 4, 4, ACT, RES, IN, OUT),          \
+      TIC_CONV3(MODE_S1, 64, 64, 1, 1, 1, ACT, RES, IN, OUT)
 
 namespace tic {
 static const ConvEntry kS1[] = {

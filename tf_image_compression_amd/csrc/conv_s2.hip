@@ -13,10 +13,18 @@ static const ConvEntry kS2[] = {
     TIC_CONV(MODE_S2, 32, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_S2, 64, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_S2, 64, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONV(MODE_S2, 64, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV3(MODE_S2, 64, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV3(MODE_S2, 64, 64, 2, 2, 2, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV3(MODE_S2, 64, 64, 4, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_S2, 64, 64, 4, 4, 1, ACT_ID, false, IN_F32, OUT_QUANT),
-    TIC_CONV(MODE_S2, 64, 64, 4, 4, 2, ACT_ID, false, IN_F32, OUT_QUANT),
+    TIC_CONV3(MODE_S2, 64, 64, 4, 4, 2, ACT_ID, false, IN_F32, OUT_QUANT),
+    TIC_CONV3(MODE_S2, 64, 64, 2, 2, 1, ACT_ID, false, IN_F32, OUT_QUANT),
+    TIC_CONV3(MODE_S2, 64, 64, 2, 2, 2, ACT_ID, false, IN_F32, OUT_QUANT),
     TIC_CONV(MODE_S2, 64, 80, 4, 4, 1, ACT_ID, false, IN_F32, OUT_QUANT),
+    TIC_PERSIST(MODE_S2, 16, 32, 4, 4, ACT_RELU),
+    TIC_PERSIST(MODE_S2, 32, 32, 4, 4, ACT_RELU),
+    TIC_PERSIST(MODE_S2, 32, 32, 2, 2, ACT_RELU),
+    TIC_PERSIST(MODE_S2, 32, 64, 2, 2, ACT_RELU),
 };
 const ConvEntry* conv_registry_s2(int* count) {
   *count = sizeof(kS2) / sizeof(kS2[0]);

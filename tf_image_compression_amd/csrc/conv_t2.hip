@@ -6,7 +6,9 @@ namespace tic {
 static const ConvEntry kT2[] = {
     TIC_CONV(MODE_T2, 64, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_T2, 64, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONV(MODE_T2, 64, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV3(MODE_T2, 64, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV3(MODE_T2, 64, 64, 2, 2, 2, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONV3(MODE_T2, 64, 64, 4, 4, 4, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_T2, 64, 32, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_T2, 64, 32, 8, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_T2, 32, 32, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
@@ -14,10 +16,17 @@ static const ConvEntry kT2[] = {
     TIC_CONV(MODE_T2, 32, 16, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_T2, 32, 16, 8, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONV(MODE_T2, 64, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_CONV(MODE_T2, 64, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
+    TIC_CONV3(MODE_T2, 64, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
+    TIC_CONV3(MODE_T2, 64, 64, 2, 2, 1, ACT_ID, false, IN_IDX, OUT_F32),
+    TIC_CONV3(MODE_T2, 64, 64, 2, 2, 2, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 80, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 80, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 64, 64, 4, 4, 1, ACT_ID, false, IN_F32, OUT_F32),
+    TIC_PERSIST(MODE_T2, 32, 32, 4, 4, ACT_RELU),
+    TIC_PERSIST(MODE_T2, 32, 32, 8, 4, ACT_RELU),
+    TIC_PERSIST(MODE_T2, 32, 16, 4, 4, ACT_RELU),
+    TIC_PERSIST(MODE_T2, 32, 16, 8, 4, ACT_RELU),
+    TIC_PERSIST(MODE_T2, 64, 32, 4, 4, ACT_RELU),
 };
 const ConvEntry* conv_registry_t2(int* count) {
   *count = sizeof(kT2) / sizeof(kT2[0]);

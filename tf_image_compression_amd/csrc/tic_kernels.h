@@ -25,6 +25,8 @@ struct ConvArgs {
   int Ho, Wo;          // output spatial
   int pad_y, pad_x;    // SAME pad_before (S1: 1; S2: 0 for even input, 1 for odd; T2: unused)
   float qscale;        // Q - 1
+  int num_cus;         // compute units (persistent variants size their grid from it)
+  int grid_cap;        // > 0: cap on the persistent grid (tests force several tiles per workgroup)
 };
 
 struct RgbInArgs {
@@ -70,7 +72,8 @@ struct ConvEntry {
   int th;             // output rows per block (input rows for T2)
   int wr;             // wave row-groups
   int nsplit;         // workgroups splitting the output channels of one pixel tile
-  int wlds;           // weights staged through LDS by LDS-DMA (1) or read from L2 (0);
+  int wlds;           // weight source: 0 L2 (prefetch 2), 1 LDS-DMA ring, 2 L2 (prefetch 6),
+                      // 3 all weights resident in LDS, persistent workgroups (conv3x3_persist.h)
   ConvLaunch fn;
 };
 

@@ -150,6 +150,7 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
     const tic::ConvEntry& c = e[i];
     if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
     if (fth && (c.th != fth || c.nsplit != fns || (fwl >= 0 && c.wlds != fwl))) continue;
+    if (c.wlds == 3 && fwl != 3) continue;  // persistent variants: only by autotune or forced
     const long wgs = (long)((wg + 15) / 16) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
     const long work = (long)c.th * 64 / c.nsplit;  // pixels x channel-fraction per workgroup
     const bool ok = wgs >= 512;
@@ -296,6 +297,7 @@ struct tic_handle {
   int num_cus = 256;
   bool use_graph = false;
   bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); measured slower, opt-in
+  int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
   struct GraphKey {
     const void *in, *idx, *rgb;
     int n, nlanes;
@@ -343,7 +345,9 @@ int check_launch() {
 }
 
 // Time `nvar` launch variants (reps each, after one warm launch) and return the fastest.
-int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(int)>& launch, int* best) {
+int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(int)>& launch, int* best,
+                  const char* label = "", int n = 0) {
+  static const bool log = getenv("TIC_TUNE_LOG") != nullptr;
   hipEvent_t t0, t1;
   HIP_TRY(hipEventCreate(&t0));
   HIP_TRY(hipEventCreate(&t1));
@@ -357,6 +361,7 @@ int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(i
     HIP_TRY(hipEventSynchronize(t1));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+    if (log) fprintf(stderr, "tune %-22s n=%d variant %d : %.2f us\n", label, n, v, 1e3f * ms / reps);
     if (ms < best_ms) {
       best_ms = ms;
       *best = v;
@@ -439,7 +444,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
         int rc = time_variants(st, tic::enc01_variants(), h->tune_reps,
                                [&](int v) { return tic::launch_enc01(d.cout, l1r.def.cout, !h->rmbe(), a, n, st, v); },
-                               &var);
+                               &var, "enc01", n);
         if (rc) return rc;
         lay.tuned_var[-n] = var;
       }
@@ -473,7 +478,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       int var = it != lay.tuned_var.end() ? it->second : kRgbInDefault;
       if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
         int rc = time_variants(st, tic::rgb_in_variants(), h->tune_reps,
-                               [&](int v) { return tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, st, v); }, &var);
+                               [&](int v) { return tic::launch_rgb_in(d.cout, !h->rmbe(), a, n, st, v); }, &var,
+                               "rgb_in", n);
         if (rc) return rc;
         lay.tuned_var[n] = var;
       }
@@ -498,7 +504,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       if (forced >= 0) var = forced;
       else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
         int rc = time_variants(st, tic::rgb_out_variants(), h->tune_reps,
-                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, st, v); }, &var);
+                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, st, v); }, &var,
+                               "rgb_out", n);
         if (rc) return rc;
         lay.tuned_var[n] = var;
       }
@@ -527,6 +534,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.Ho = a.Wo = lay.h_out;
       a.pad_y = a.pad_x = same_pad(d.kind, lay.h_in);
       a.qscale = (float)(h->Q - 1);
+      a.num_cus = h->num_cus;
+      a.grid_cap = h->persist_grid;
       if (h->tune_reps > 0 && it == lay.tuned.end()) {
         // time every compiled tiling on the live buffers (re-launching is idempotent)
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
@@ -994,6 +1003,12 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->fuse01 = value != 0;
     return TIC_OK;
   }
+  if (k == "persist_grid") {
+    if (value < 0) return fail(TIC_EINVAL, "persist_grid must be >= 0");
+    clear_graphs(h);
+    h->persist_grid = value;
+    return TIC_OK;
+  }
   if (k == "graph") {
     h->use_graph = value != 0;
     return TIC_OK;
@@ -1150,6 +1165,134 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
   return TIC_OK;
 }
 
+// In-situ tuning: per-layer variant choice by the time of the WHOLE launch sequence as
+// it really runs (both lanes concurrently), not of the layer alone.  Greedy coordinate
+// descent over the layers, `rounds` passes; every candidate is bit-identical (tap-major
+// order; dense last layer), so only speed changes.  Starts from the solo-tuned (or
+// default) choice of each layer.
+int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int reps) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!d_in || n <= 0 || rounds <= 0 || reps <= 0) return fail(TIC_EINVAL, "bad arguments");
+  if (n > h->chunk) return fail(TIC_EINVAL, "autotune_step n %d exceeds chunk %d", n, h->chunk);
+  // per-launch batch sizes the lanes will see for n
+  std::vector<int> sizes;
+  if (h->nlanes >= 2 && n >= 2) {
+    sizes.push_back((n + 1) / 2);
+    if (n / 2 != (n + 1) / 2) sizes.push_back(n / 2);
+  } else {
+    sizes.push_back(n);
+  }
+  // make sure every layer has a solo-tuned starting point for those sizes
+  for (int m : sizes) {
+    bool have = true;
+    for (size_t i = 0; i < h->layers.size(); ++i) {
+      const LayerRT& l = h->layers[i];
+      const bool rgb = i == 0 || i + 1 == h->layers.size();
+      if (rgb ? !l.tuned_var.count(m) : !l.tuned.count(m)) have = false;
+    }
+    if (!have) {
+      rc = tic_autotune(h, d_in, m, reps);
+      if (rc) return rc;
+    }
+  }
+  clear_graphs(h);
+  void *d_idx = nullptr, *d_out = nullptr;
+  const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
+  const size_t px = (size_t)n * h->P * h->P * 3;
+  HIP_TRY(hipMalloc(&d_idx, std::max<size_t>(ce, 16)));
+  HIP_TRY(hipMalloc(&d_out, px * (h->rmbe() ? 4 : 1)));
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  HIP_TRY(hipEventCreate(&t0));
+  HIP_TRY(hipEventCreate(&t1));
+  auto step = [&]() {
+    return h->rmbe() ? rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr})
+                     : codec_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, (uint8_t*)d_out);
+  };
+  auto measure = [&](float* best) -> int {
+    *best = 1e30f;
+    int r = step();  // warm
+    if (r) return r;
+    for (int k = 0; k < 3; ++k) {
+      HIP_TRY(hipEventRecord(t0, h->stream));
+      for (int q = 0; q < reps; ++q) {
+        r = step();
+        if (r) return r;
+      }
+      HIP_TRY(hipEventRecord(t1, h->stream));
+      HIP_TRY(hipEventSynchronize(t1));
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+      *best = std::min(*best, ms / reps);
+    }
+    return TIC_OK;
+  };
+  const bool log = getenv("TIC_TUNE_LOG") != nullptr;
+  float cur = 0.f;
+  rc = measure(&cur);
+  if (log && !rc) fprintf(stderr, "tune-step n=%d start: %.2f us\n", n, 1e3f * cur);
+  const int L = (int)h->layers.size();
+  for (int round = 0; round < rounds && !rc; ++round) {
+    for (int i = 0; i < L && !rc; ++i) {
+      LayerRT& l = h->layers[i];
+      const LayerDef& d = l.def;
+      const bool first = i == 0, last = i == L - 1;
+      if ((first || i == 1) && fuses01(h)) continue;
+      if (last && rgb_out_forced() >= 0) continue;
+      if (first || last) {
+        const int nv = first ? tic::rgb_in_variants() : tic::rgb_out_variants();
+        const int keep = l.tuned_var[sizes[0]];
+        int best_v = keep;
+        float best = cur;
+        for (int v = 0; v < nv && !rc; ++v) {
+          if (v == keep) continue;
+          for (int m : sizes) l.tuned_var[m] = v;
+          float ms = 0.f;
+          rc = measure(&ms);
+          if (log) fprintf(stderr, "tune-step %-22s variant %d : %.2f us\n", d.name.c_str(), v, 1e3f * ms);
+          if (!rc && ms < best) {
+            best = ms;
+            best_v = v;
+          }
+        }
+        for (int m : sizes) l.tuned_var[m] = best_v;
+        cur = best;
+      } else {
+        const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
+        auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
+                                     last_enc ? tic::OUT_QUANT : tic::OUT_F32);
+        const tic::ConvEntry* keep = l.tuned[sizes[0]];
+        const tic::ConvEntry* best_e = keep;
+        float best = cur;
+        for (const tic::ConvEntry* c : cands) {
+          if (c == keep || rc) continue;
+          for (int m : sizes) l.tuned[m] = c;
+          float ms = 0.f;
+          rc = measure(&ms);
+          if (log)
+            fprintf(stderr, "tune-step %-22s th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), c->th, c->nsplit,
+                    c->wlds, 1e3f * ms);
+          if (!rc && ms < best) {
+            best = ms;
+            best_e = c;
+          }
+        }
+        for (int m : sizes) l.tuned[m] = best_e;
+        cur = best;
+      }
+    }
+    if (log && !rc) fprintf(stderr, "tune-step n=%d after round %d: %.2f us\n", n, round + 1, 1e3f * cur);
+  }
+  hipError_t e = hipStreamSynchronize(h->stream);
+  (void)hipEventDestroy(t0);
+  (void)hipEventDestroy(t1);
+  (void)hipFree(d_idx);
+  (void)hipFree(d_out);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(TIC_EHIP, "autotune_step sync: %s", hipGetErrorString(e));
+  return TIC_OK;
+}
+
 int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
   if (!h || !th || !nsplit) return fail(TIC_EINVAL, "null argument");
   // nsplit reports (channel split) + 100 * (weights via LDS)
@@ -1216,8 +1359,12 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
                             : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
                                         last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n);
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
-    snprintf(buf, sizeof buf, "conv3x3<%d,%d,%d,%d,%d,%d,%s,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th, e->wr,
-             e->nsplit, tf[e->wlds != 0], e->act, tf[e->res != 0], e->in, e->out);
+    if (e->wlds == 3)
+      snprintf(buf, sizeof buf, "conv3x3_persist_kernel<%d,%d,%d,%d,%d,%d>", e->mode, e->cin, e->cout, e->th, e->wr,
+               e->act);
+    else
+      snprintf(buf, sizeof buf, "conv3x3<%d,%d,%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th,
+               e->wr, e->nsplit, e->wlds, e->act, tf[e->res != 0], e->in, e->out);
   }
   const int len = (int)strlen(buf);
   if (len + 1 > cap) return fail(TIC_EINVAL, "name buffer too small (%d < %d)", cap, len + 1);
@@ -1256,6 +1403,8 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.Wo = out_size(kind, W);
   a.pad_y = same_pad(kind, H);
   a.pad_x = same_pad(kind, W);
+  a.num_cus = h->num_cus;
+  a.grid_cap = h->persist_grid;
   e->fn(a, n, h->stream);
   int rc = check_launch();
   hipError_t se = hipStreamSynchronize(h->stream);
