@@ -1,9 +1,10 @@
+# Round validation on the GPU box: parity tests, default bench, rocprofv3 kernel stats.
 set -e
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-timeout -k 10 240 python tools/ab.py --rounds 5 --cfg streams=2,graph=0 --cfg streams=2,graph=1 > gpurun_out/ab_graph.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench_v3.json 2> gpurun_out/bench_v3.err
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r01}
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 300 python bench.py --layers-out gpurun_out/bench_layers_$TAG.json > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_v3 -o p -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --steps 20 > $GRAFT_REPO_ROOT/gpurun_out/prof_v3.log 2>&1
-cd $GRAFT_REPO_ROOT
-bash tools/pmc_box.sh
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o p -- python3 $R/bench.py --no-cpu-baseline --steps 20 > $R/gpurun_out/prof_$TAG.log 2>&1
