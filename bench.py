@@ -47,7 +47,16 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic")
     ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
-    return ap.parse_args()
+    ap.add_argument("--workload", choices=["patches", "image4k"], default="patches",
+                    help="patches: BASELINE configs[1]/[2] (default); image4k: configs[4], whole "
+                         "3840x2160 images tiled 256x256 -> model_3 -> stitch -> rmbe post-filter -> u8")
+    ap.add_argument("--images", type=int, default=1, help="image4k: images per rank per step")
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    args = ap.parse_args()
+    if args.workload == "image4k" and "--model" not in sys.argv:
+        args.model = 3
+    return args
 
 
 def kernel_groups(codec, model_id, P, ms):
@@ -149,6 +158,8 @@ def parity_probe(codec, model_id, P, params, mean, std):
 
 def main():
     args = parse()
+    if args.workload == "image4k":
+        return main_image(args)
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
     from tf_image_compression_amd.topology import bottleneck_shape, layer_table
@@ -269,6 +280,174 @@ def main():
             out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     comm.close()
+    codec.close()
+
+
+def cpu_baseline_image(model_id, P, params, mean, std, rparams, H, W, target_s):
+    """Oracle (float32, OpenBLAS) on a bounded sample — 2 codec patches + 4 rmbe windows,
+    timed repeatedly — extrapolated to one HxW image (patch and window counts of the
+    image); the reference's TF-CPU path cannot run here."""
+    from oracle import tic_oracle as o
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    cores = min(16, os.cpu_count() or 1)
+    n_p, n_w = 2, 4
+    r = np.random.default_rng(98)
+    x = r.integers(0, 256, (n_p, P, P, 3), dtype=np.uint8)
+    win = r.random((n_w, 128, 128, 3), dtype=np.float32) * 255
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    tp, tw = [], []
+    try:
+        t_begin = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            _, idx = o.encoder(params, mean, std, x, P, 2, model_id, acc=np.float32)
+            o.decoder(params, mean, std, idx, 2, model_id, acc=np.float32)
+            t1 = time.perf_counter()
+            o.rmbe_model(rparams, mean, std, win, acc=np.float32)
+            tw.append(time.perf_counter() - t1)
+            tp.append(t1 - t0)
+            if time.perf_counter() - t_begin > target_s and len(tp) >= 2:
+                break
+    finally:
+        if ctx is not None and hasattr(ctx, "unregister"):
+            ctx.unregister()
+    hn, wn = -(-H // P), -(-W // P)
+    n_win = (H // 128) * ((W - 64) // 128) + ((H - 64) // 128) * (W // 128)
+    t_img = float(np.median(tp)) / n_p * hn * wn + float(np.median(tw)) / n_w * n_win
+    return {"value": round(H * W / t_img / 1e6, 4), "unit": "MPix/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/tic_oracle.py float32 (OpenBLAS {cores} threads): model_{model_id} "
+                      f"{n_p} x {P}x{P} patches encode+decode and rmbe {n_w} x 128x128 windows, median of "
+                      f"{len(tp)} runs, extrapolated to {hn * wn} patches + {n_win} windows of one "
+                      f"{W}x{H} image"}
+
+
+def main_image(args):
+    """BASELINE configs[4]: whole images, device-resident from the uint8 image to the uint8
+    reconstruction: reflect tiling -> model encode -> decode (f32) -> stitch -> rmbe
+    (2 window passes) -> np.around -> uint8.  One step = args.images images per rank."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.image_codec import ImageCodec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import bottleneck_shape, RMBE_ID
+    from tf_image_compression_amd import dist
+
+    rank, world, local = dist.env_rank()
+    P, M, H, W, NI = args.patch, args.model, args.height, args.width, args.images
+    params = synthetic_params(M, seed=0)
+    rparams = synthetic_params(RMBE_ID, seed=0)
+    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local)
+    post = Codec(RMBE_ID, rparams, SYNTH_MEAN, SYNTH_STD, patch_size=128, device=local)
+    for c in (codec, post):
+        c.set_option("streams", args.streams)
+    comm = dist.make_comm(codec)
+    ic = ImageCodec(codec, post)
+    eh, ew, ec = bottleneck_shape(M, P)
+    npat = ic.num_patches(H, W)
+    r = np.random.default_rng(1234 + rank)
+    imgs = [r.integers(0, 256, (H, W, 3), dtype=np.uint8) for _ in range(NI)]
+    d_img = [codec.alloc(H * W * 3) for _ in range(NI)]
+    for d, x in zip(d_img, imgs):
+        d.upload(x)
+    d_sym = [codec.alloc(npat * eh * ew * ec) for _ in range(NI)]
+    d_out = [codec.alloc(H * W * 3) for _ in range(NI)]
+
+    lane_b = (npat + 1) // 2 if args.streams == 2 else npat
+    n_win = (H // 128) * ((W - 64) // 128) + ((H - 64) // 128) * (W // 128)
+    win_lane = (min(n_win, 256) + 1) // 2 if args.streams == 2 else min(n_win, 256)
+    d_pat = codec.alloc(npat * P * P * 3)
+    codec.image_to_patches_device(d_img[0], H, W, P, d_pat)
+    d_win = post.alloc(win_lane * 128 * 128 * 3 * 4)
+    d_win.upload(r.random((win_lane, 128, 128, 3), dtype=np.float32) * 255)
+    if not args.no_autotune:
+        codec.autotune(d_pat, lane_b, reps=5)
+        post.autotune(d_win, win_lane, reps=5)
+
+    def step():
+        for i in range(NI):
+            ic.roundtrip_device(d_img[i], H, W, d_sym[i], d_out[i], post_filter=True)
+
+    for _ in range(args.warmup):
+        step()
+    ic.synchronize()
+    comm.barrier()
+    ic.synchronize()
+    t0 = time.perf_counter()
+    wall0 = time.time()
+    for _ in range(args.steps):
+        step()
+    ic.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    wall1 = time.time()
+    t_max = comm.allreduce_max(elapsed)
+
+    sse = 0.0
+    for d, x in zip(d_out, imgs):
+        rec = d.download(x.shape, np.uint8)
+        sse += float(np.sum(np.square(rec.astype(np.float64) - x.astype(np.float64))))
+    st = dist.RankStats(sse=sse * args.steps, dims=NI * H * W * 3 * args.steps,
+                        bits=NI * npat * eh * ew * ec * args.steps, images=NI * args.steps,
+                        t_start=wall0, t_end=wall1)
+    summary = dist.combine(comm.allgather_stats(st))
+
+    # per-layer HIP-event timing of both networks at their per-launch batch sizes
+    ms_c = codec.profile_layers(d_pat, lane_b, args.profile_iters)
+    ms_r = post.profile_layers(d_win, win_lane, args.profile_iters)
+    groups, rows = kernel_groups(codec, M, P, ms_c)
+    rgroups, rrows = kernel_groups(post, RMBE_ID, 128, ms_r)
+    # dominant = largest time per image: per-launch ms x launches per image
+    per_img = {("codec",) + k: (g, lane_b, npat) for k, g in groups.items()}
+    per_img.update({("rmbe",) + k: (g, win_lane, n_win) for k, g in rgroups.items()})
+    dom_key = max(per_img, key=lambda k: per_img[k][0]["ms"] * per_img[k][2] / per_img[k][1])
+    g, lb, _ = per_img[dom_key]
+    roof, dom_ms, _, _ = roofline_of(g, lb)
+    roof["traffic"] = None
+    roof["traffic_source"] = None
+    roof["kernel"] = ("rmbe:" if dom_key[0] == "rmbe" else f"model_{M}:") + "+".join(g["layers"])
+    roof["ms_per_launch"] = round(dom_ms, 5)
+    # step roofline: both networks' layers at the image's patch / window counts
+    t_min = 0.0
+    for rr, cnt in [(rows, npat), (rrows, n_win)]:
+        for x in rr:
+            t_min += max(x["flops_per_patch"] * cnt / (PEAK_FP32_TFLOPS * 1e12),
+                         (x["bytes_per_patch"] * cnt + x["weight_bytes"]) / (PEAK_HBM_GBS * 1e9))
+    step_ms = t_max * 1e3 / args.steps
+    value = world * NI * H * W * args.steps / t_max / 1e6
+    out = {
+        "metric": "encode+decode MPix/s at 256x256 RGB",
+        "value": round(value, 2),
+        "unit": "MPix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic uniform u8 images (seed 1234+rank), seeded He-normal weights",
+        "config": {"workload": f"model_{M} + rmbe post-filter, {NI} x {W}x{H} RGB image(s) per GPU tiled "
+                               f"{P}x{P} ({npat} patches, {n_win} rmbe windows per image)",
+                   "model": f"model_{M}+rmbe", "images_per_gpu": NI, "image": [H, W], "patch": P,
+                   "code_shape": [eh, ew, ec], "parallelism": f"image-parallel x{world}"},
+        "roofline": roof,
+        "roofline_step_frac": round(t_min * NI * 1e3 / step_ms, 4),
+        "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "windows_per_launch": win_lane},
+        "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
+                            "raw_bpp": round(summary["bpp"], 4)},
+    }
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_image(M, P, params, SYNTH_MEAN, SYNTH_STD, rparams, H, W,
+                                                     args.cpu_seconds)
+            out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    ic.close()
+    comm.close()
+    post.close()
     codec.close()
 
 

@@ -154,6 +154,49 @@ int tic_get_stream(tic_handle* h, void** stream);
 /* Device info string (name, CUs, arch) for logs. */
 int tic_device_info(tic_handle* h, char* buf, int len);
 
+/* --- whole images (BASELINE config 5) and symbol statistics; device pointers, async on
+ * the handle's stream.  Any handle may run the glue kernels; tic_rmbe_image_device needs
+ * a TIC_MODEL_RMBE handle. --- */
+
+/* Reflect-pad an HWC uint8 image [H,W,3] bottom/right to multiples of P (np.pad 'reflect':
+ * edge pixel not repeated, any pad length) and cut row-major PxP patches into
+ * d_patches [ceil(H/P)*ceil(W/P), P, P, 3] (4-byte aligned; P a multiple of 4).
+ * Replaces: utils.crop_image_input_patches (utils/utils.py:96-133), encode.py:154-156. */
+int tic_image_to_patches_device(tic_handle* h, const uint8_t* d_img, int H, int W, int P, uint8_t* d_patches);
+
+/* Stitch row-major float32 patches [ceil(H/P)*ceil(W/P), P, P, 3] into an HWC image cropped
+ * to HxW.  Replaces: utils.concat_patches (utils/utils.py:136-167), decode.py:222-230. */
+int tic_patches_to_image_device(tic_handle* h, const float* d_patches, int H, int W, int P, float* d_img);
+
+/* Block-effect post-filter of a whole float32 HWC image [H,W,3] in [0,255], in place: the
+ * 128x128 windows at column offset 64 (all full rows of windows), filtered and written back,
+ * then the windows at row offset 64; edge strips that fill no window stay untouched.
+ * Replaces: rmbe.rmbe / rmbe_height / rmbe_width (submit/2/rmbe/rmbe.py:15-111) with the
+ * network of submit/2/rmbe/model.py:113-197 (one handle, no per-call graph rebuild). */
+int tic_rmbe_image_device(tic_handle* h, float* d_img, int H, int W);
+
+/* np.around(x).astype(np.uint8) of n float32 values in [0,255] (half to even; clamped).
+ * Replaces: submit/2/decoder.py:176, decode.py:249. */
+int tic_round_u8_device(tic_handle* h, const float* d_in, size_t n, uint8_t* d_out);
+
+/* Accumulate np.histogram(symbols, bins=range(Q+1))[0] of n uint8 symbols into the uint64
+ * counts d_counts[Q] (d_sym 4-byte aligned, d_counts 8-byte aligned; zero it first with
+ * tic_memset_device).  Replaces: get_encoded_distribution.py:113-126 (the per-batch
+ * histogram of the encoder output summed over the data set). */
+int tic_histogram_device(tic_handle* h, const uint8_t* d_sym, size_t n, int Q, uint64_t* d_counts);
+
+/* Accumulate the exact sum of squared differences of two uint8 arrays of n bytes into
+ * *d_acc (uint64; 4-byte aligned inputs).  Replaces: evaluate.mse summed over a data set
+ * (processing_utils/evaluate.py:10-32; dataset PSNR = 10 log10(255^2 sum(dims)/sum(SSE))). */
+int tic_sse_u8_device(tic_handle* h, const uint8_t* d_a, const uint8_t* d_b, size_t n, uint64_t* d_acc);
+
+/* hipMemsetAsync on the handle's stream. */
+int tic_memset_device(tic_handle* h, void* d_ptr, int value, size_t bytes);
+
+/* Make `waiter`'s stream wait for all work enqueued so far on `signaler`'s stream (same
+ * device): chains a codec handle and an rmbe handle without a host synchronisation. */
+int tic_stream_wait(tic_handle* waiter, tic_handle* signaler);
+
 /* --- entropy coder (host, no device) ---
  * Replaces the third-party `range_coder` package used by encode.py:86-97 and
  * decode.py:89-99: RangeEncoder(path).encode(data, cum_freq) / .close() and

@@ -57,6 +57,14 @@ SIGNATURES = [
     ("tic_conv3x3_device", C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      f32p, f32p, vp, vp]),
     ("tic_get_stream", C.c_int, [vp, C.POINTER(vp)]),
+    ("tic_image_to_patches_device", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
+    ("tic_patches_to_image_device", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
+    ("tic_rmbe_image_device", C.c_int, [vp, vp, C.c_int, C.c_int]),
+    ("tic_round_u8_device", C.c_int, [vp, vp, C.c_size_t, vp]),
+    ("tic_histogram_device", C.c_int, [vp, vp, C.c_size_t, C.c_int, vp]),
+    ("tic_sse_u8_device", C.c_int, [vp, vp, vp, C.c_size_t, vp]),
+    ("tic_memset_device", C.c_int, [vp, vp, C.c_int, C.c_size_t]),
+    ("tic_stream_wait", C.c_int, [vp, vp]),
     # entropy coder (host only)
     ("tic_rc_last_error", C.c_char_p, []),
     ("tic_rc_encoder_open", C.c_int, [C.c_char_p, C.POINTER(vp)]),

@@ -214,6 +214,34 @@ class Codec:
                                        ptr(b, C.c_float), d_res.ptr if d_res else None, d_out.ptr),
               "tic_conv3x3_device")
 
+    # ------------------------------------------------------------------ whole images (image_ops.hip)
+    def image_to_patches_device(self, d_img: DeviceBuffer, H: int, W: int, P: int, d_patches: DeviceBuffer):
+        check(lib().tic_image_to_patches_device(self._h, d_img.ptr, H, W, P, d_patches.ptr),
+              "tic_image_to_patches_device")
+
+    def patches_to_image_device(self, d_patches: DeviceBuffer, H: int, W: int, P: int, d_img: DeviceBuffer):
+        check(lib().tic_patches_to_image_device(self._h, d_patches.ptr, H, W, P, d_img.ptr),
+              "tic_patches_to_image_device")
+
+    def rmbe_image_device(self, d_img: DeviceBuffer, H: int, W: int):
+        check(lib().tic_rmbe_image_device(self._h, d_img.ptr, H, W), "tic_rmbe_image_device")
+
+    def round_u8_device(self, d_in: DeviceBuffer, n: int, d_out: DeviceBuffer):
+        check(lib().tic_round_u8_device(self._h, d_in.ptr, n, d_out.ptr), "tic_round_u8_device")
+
+    def histogram_device(self, d_sym: DeviceBuffer, n: int, Q: int, d_counts: DeviceBuffer):
+        check(lib().tic_histogram_device(self._h, d_sym.ptr, n, Q, d_counts.ptr), "tic_histogram_device")
+
+    def sse_u8_device(self, d_a: DeviceBuffer, d_b: DeviceBuffer, n: int, d_acc: DeviceBuffer):
+        check(lib().tic_sse_u8_device(self._h, d_a.ptr, d_b.ptr, n, d_acc.ptr), "tic_sse_u8_device")
+
+    def memset_device(self, d: DeviceBuffer, value: int, nbytes: int):
+        check(lib().tic_memset_device(self._h, d.ptr, value, nbytes), "tic_memset_device")
+
+    def wait_for(self, other: "Codec") -> None:
+        """Order this handle's stream after everything enqueued so far on ``other``'s."""
+        check(lib().tic_stream_wait(self._h, other._h), "tic_stream_wait")
+
     # ------------------------------------------------------------------ lifetime
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

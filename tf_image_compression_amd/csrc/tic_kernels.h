@@ -91,4 +91,15 @@ int rgb_out_variants();
 bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant);
 bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant);
 
+// Whole-image glue and the symbol histogram (image_ops.hip).
+void launch_tile_reflect(const uint8_t* img, int H, int W, int P, int hn, int wn, uint8_t* out, int num_cus,
+                         hipStream_t s);
+void launch_stitch(const float* patches, int H, int W, int P, int wn, float* img, int num_cus, hipStream_t s);
+void launch_window_copy(float* img, int W, int r0, int c0, int S, int hn, int wn, float* win, bool to_windows,
+                        int num_cus, hipStream_t s);
+void launch_round_u8(const float* in, size_t n, uint8_t* out, int num_cus, hipStream_t s);
+void launch_sse_u8(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* acc, int num_cus,
+                   hipStream_t s);
+void launch_histogram(const uint8_t* sym, size_t n, int Q, unsigned long long* counts, int num_cus, hipStream_t s);
+
 }  // namespace tic

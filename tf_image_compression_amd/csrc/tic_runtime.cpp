@@ -292,6 +292,12 @@ struct tic_handle {
   size_t st_out_bytes = 0;
   void* st_out2 = nullptr;
   size_t st_out2_bytes = 0;
+  // whole-image post-filter scratch (tic_rmbe_image_device): windows in / out
+  void* win_in = nullptr;
+  size_t win_in_bytes = 0;
+  void* win_out = nullptr;
+  size_t win_out_bytes = 0;
+  hipEvent_t ev_dep = nullptr;  // tic_stream_wait
   std::vector<void*> user_allocs;
   int tune_reps = 0;  // > 0 while tic_autotune runs
   int num_cus = 256;
@@ -791,6 +797,9 @@ void tic_destroy(tic_handle* h) {
   if (h->st_in) (void)hipFree(h->st_in);
   if (h->st_out) (void)hipFree(h->st_out);
   if (h->st_out2) (void)hipFree(h->st_out2);
+  if (h->win_in) (void)hipFree(h->win_in);
+  if (h->win_out) (void)hipFree(h->win_out);
+  if (h->ev_dep) (void)hipEventDestroy(h->ev_dep);
   for (void* p : h->user_allocs) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1427,6 +1436,105 @@ int tic_device_info(tic_handle* h, char* buf, int len) {
   HIP_TRY(hipGetDeviceProperties(&p, h->device));
   snprintf(buf, len, "%s | %s | CUs %d | HBM %.1f GB | device %d", p.name, p.gcnArchName, p.multiProcessorCount,
            p.totalGlobalMem / 1e9, h->device);
+  return TIC_OK;
+}
+
+
+// ---- whole images (BASELINE config 5) and the symbol histogram: image_ops.hip ----
+
+int tic_image_to_patches_device(tic_handle* h, const uint8_t* d_img, int H, int W, int P, uint8_t* d_patches) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (H <= 0 || W <= 0 || P < 4 || P % 4 != 0 || !d_img || !d_patches)
+    return fail(TIC_EINVAL, "bad arguments (H %d, W %d, P %d; P must be a positive multiple of 4)", H, W, P);
+  if (((uintptr_t)d_patches & 3) != 0) return fail(TIC_EINVAL, "d_patches must be 4-byte aligned");
+  HIP_TRY(hipSetDevice(h->device));
+  const int hn = (H + P - 1) / P, wn = (W + P - 1) / P;
+  tic::launch_tile_reflect(d_img, H, W, P, hn, wn, d_patches, h->num_cus, h->stream);
+  return check_launch();
+}
+
+int tic_patches_to_image_device(tic_handle* h, const float* d_patches, int H, int W, int P, float* d_img) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (H <= 0 || W <= 0 || P <= 0 || !d_img || !d_patches) return fail(TIC_EINVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(h->device));
+  tic::launch_stitch(d_patches, H, W, P, (W + P - 1) / P, d_img, h->num_cus, h->stream);
+  return check_launch();
+}
+
+int tic_rmbe_image_device(tic_handle* h, float* d_img, int H, int W) {
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!h->rmbe()) return fail(TIC_EINVAL, "handle is not an rmbe handle");
+  if (H <= 0 || W <= 0 || !d_img) return fail(TIC_EINVAL, "bad arguments");
+  const int S = h->P, off = S / 2;  // submit/2/rmbe/rmbe.py:12 (128) and :16 (64)
+  struct Pass { int r0, c0, hn, wn; };
+  const Pass passes[2] = {{0, off, H / S, (W - off) / S},    // rmbe_height :70-89
+                          {off, 0, (H - off) / S, W / S}};   // rmbe_width  :92-111
+  for (const Pass& ps : passes) {
+    if (ps.hn <= 0 || ps.wn <= 0) continue;
+    const int n = ps.hn * ps.wn;
+    const size_t bytes = (size_t)n * S * S * 3 * sizeof(float);
+    rc = ensure(&h->win_in, &h->win_in_bytes, bytes);
+    if (!rc) rc = ensure(&h->win_out, &h->win_out_bytes, bytes);
+    if (rc) return rc;
+    tic::launch_window_copy(d_img, W, ps.r0, ps.c0, S, ps.hn, ps.wn, (float*)h->win_in, true, h->num_cus, h->stream);
+    if ((rc = check_launch())) return rc;
+    rc = rmbe_dev(h, (const float*)h->win_in, n, (float*)h->win_out, Prof{nullptr});
+    if (rc) return rc;
+    tic::launch_window_copy(d_img, W, ps.r0, ps.c0, S, ps.hn, ps.wn, (float*)h->win_out, false, h->num_cus,
+                            h->stream);
+    if ((rc = check_launch())) return rc;
+  }
+  return TIC_OK;
+}
+
+int tic_round_u8_device(tic_handle* h, const float* d_in, size_t n, uint8_t* d_out) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (n == 0) return TIC_OK;
+  if (!d_in || !d_out) return fail(TIC_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  tic::launch_round_u8(d_in, n, d_out, h->num_cus, h->stream);
+  return check_launch();
+}
+
+int tic_histogram_device(tic_handle* h, const uint8_t* d_sym, size_t n, int Q, uint64_t* d_counts) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (Q < 1 || Q > 256) return fail(TIC_EINVAL, "Q %d must be in [1, 256]", Q);
+  if (n == 0) return TIC_OK;
+  if (!d_sym || !d_counts) return fail(TIC_EINVAL, "null argument");
+  if (((uintptr_t)d_sym & 3) != 0 || ((uintptr_t)d_counts & 7) != 0)
+    return fail(TIC_EINVAL, "d_sym must be 4-byte and d_counts 8-byte aligned");
+  HIP_TRY(hipSetDevice(h->device));
+  tic::launch_histogram(d_sym, n, Q, reinterpret_cast<unsigned long long*>(d_counts), h->num_cus, h->stream);
+  return check_launch();
+}
+
+int tic_sse_u8_device(tic_handle* h, const uint8_t* d_a, const uint8_t* d_b, size_t n, uint64_t* d_acc) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (n == 0) return TIC_OK;
+  if (!d_a || !d_b || !d_acc) return fail(TIC_EINVAL, "null argument");
+  if (((uintptr_t)d_a & 3) != 0 || ((uintptr_t)d_b & 3) != 0 || ((uintptr_t)d_acc & 7) != 0)
+    return fail(TIC_EINVAL, "d_a / d_b must be 4-byte and d_acc 8-byte aligned");
+  HIP_TRY(hipSetDevice(h->device));
+  tic::launch_sse_u8(d_a, d_b, n, reinterpret_cast<unsigned long long*>(d_acc), h->num_cus, h->stream);
+  return check_launch();
+}
+
+int tic_memset_device(tic_handle* h, void* d_ptr, int value, size_t bytes) {
+  if (!h || (!d_ptr && bytes)) return fail(TIC_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemsetAsync(d_ptr, value, bytes, h->stream));
+  return TIC_OK;
+}
+
+int tic_stream_wait(tic_handle* waiter, tic_handle* signaler) {
+  if (!waiter || !signaler) return fail(TIC_EINVAL, "null handle");
+  if (waiter == signaler) return TIC_OK;
+  if (waiter->device != signaler->device) return fail(TIC_EINVAL, "handles on different devices");
+  HIP_TRY(hipSetDevice(signaler->device));
+  if (!signaler->ev_dep) HIP_TRY(hipEventCreateWithFlags(&signaler->ev_dep, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(signaler->ev_dep, signaler->stream));
+  HIP_TRY(hipStreamWaitEvent(waiter->stream, signaler->ev_dep, 0));
   return TIC_OK;
 }
 

@@ -1,0 +1,134 @@
+"""Whole-image encode / decode on one GPU (BASELINE config 5), device-resident end to end.
+
+The reference does the image plumbing on the host between ``sess.run`` calls:
+``utils.crop_image_input_patches`` (utils/utils.py:96-133) before the encoder,
+``utils.concat_patches`` (:136-167) after the decoder, then for CLIC submission 2 the
+block-effect post-filter ``rmbe.rmbe`` (submit/2/rmbe/rmbe.py:15-111) and
+``np.around(...).astype(np.uint8)`` (submit/2/decoder.py:176; decode.py:249).  Here every
+one of those steps is a kernel on the codec's stream (image_ops.hip), the rmbe network
+runs on its own handle, and the two streams are chained with an event
+(``Codec.wait_for``) instead of a host synchronisation.  Host memory is touched only to
+upload the uint8 image / symbols and download the result.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .codec import Codec, DeviceBuffer
+
+
+class ImageCodec:
+    """``codec``: a model_N Codec; ``post``: optional rmbe Codec (TIC_MODEL_RMBE)."""
+
+    def __init__(self, codec: Codec, post: Codec | None = None):
+        self.codec = codec
+        self.post = post
+        self._bufs: dict[str, DeviceBuffer] = {}
+
+    # ------------------------------------------------------------------ geometry
+    def grid(self, H: int, W: int) -> tuple[int, int]:
+        """Patches per column / row (utils/utils.py:100-113: pad up to a multiple of P)."""
+        P = self.codec.patch_size
+        return -(-H // P), -(-W // P)
+
+    def num_patches(self, H: int, W: int) -> int:
+        hn, wn = self.grid(H, W)
+        return hn * wn
+
+    def _buf(self, key: str, nbytes: int, owner: Codec | None = None) -> DeviceBuffer:
+        b = self._bufs.get(key)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+            b = (owner or self.codec).alloc(max(int(nbytes), 16))
+            self._bufs[key] = b
+        return b
+
+    # ------------------------------------------------------------------ device pipeline
+    def encode_image_device(self, d_img: DeviceBuffer, H: int, W: int, d_sym: DeviceBuffer) -> int:
+        """uint8 HWC image (device) -> symbols [n, eh, ew, ec] (device).  Returns n."""
+        P = self.codec.patch_size
+        n = self.num_patches(H, W)
+        d_pat = self._buf("patches_u8", n * P * P * 3)
+        self.codec.image_to_patches_device(d_img, H, W, P, d_pat)
+        self.codec.encode_device(d_pat, n, d_sym)
+        return n
+
+    def decode_image_device(self, d_sym: DeviceBuffer, H: int, W: int, d_out: DeviceBuffer,
+                            post_filter: bool = True) -> None:
+        """symbols (device) -> uint8 HWC image [H, W, 3] (device)."""
+        P = self.codec.patch_size
+        n = self.num_patches(H, W)
+        d_f = self._buf("patches_f32", n * P * P * 3 * 4)
+        d_img = self._buf("image_f32", H * W * 3 * 4)
+        self.codec.decode_device(d_sym, n, None, d_f)
+        self.codec.patches_to_image_device(d_f, H, W, P, d_img)
+        if post_filter and self.post is not None:
+            self.post.wait_for(self.codec)
+            self.post.rmbe_image_device(d_img, H, W)
+            self.post.round_u8_device(d_img, H * W * 3, d_out)
+            self.codec.wait_for(self.post)  # later codec work may reuse the buffers
+        else:
+            self.codec.round_u8_device(d_img, H * W * 3, d_out)
+
+    def roundtrip_device(self, d_img: DeviceBuffer, H: int, W: int, d_sym: DeviceBuffer, d_out: DeviceBuffer,
+                         post_filter: bool = True) -> None:
+        self.encode_image_device(d_img, H, W, d_sym)
+        self.decode_image_device(d_sym, H, W, d_out, post_filter)
+
+    def synchronize(self) -> None:
+        self.codec.synchronize()
+        if self.post is not None:
+            self.post.synchronize()
+
+    # ------------------------------------------------------------------ host entry points
+    def encode_image(self, image: np.ndarray) -> np.ndarray:
+        """uint8 [H, W, 3] -> uint8 symbols [n, eh, ew, ec] (encode.py:154-182)."""
+        img = np.ascontiguousarray(image)
+        if img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] != 3:
+            raise ValueError(f"image must be uint8 [H, W, 3], got {img.dtype} {img.shape}")
+        H, W, _ = img.shape
+        eh, ew, ec = self.codec.code_shape
+        n = self.num_patches(H, W)
+        d_img = self._buf("image_u8", img.nbytes)
+        d_img.upload(img)
+        d_sym = self._buf("symbols", n * eh * ew * ec)
+        self.encode_image_device(d_img, H, W, d_sym)
+        return d_sym.download((n, eh, ew, ec), np.uint8)
+
+    def decode_image(self, symbols: np.ndarray, H: int, W: int, post_filter: bool = True) -> np.ndarray:
+        """uint8 symbols [n, eh, ew, ec] -> uint8 [H, W, 3] (decode.py:204-249,
+        submit/2/decoder.py:150-176 with the post-filter)."""
+        eh, ew, ec = self.codec.code_shape
+        n = self.num_patches(H, W)
+        s = np.ascontiguousarray(symbols, np.uint8).reshape(-1, eh, ew, ec)
+        if s.shape[0] != n:
+            raise ValueError(f"{s.shape[0]} patches of symbols for a {H}x{W} image (expected {n})")
+        if s.size and int(s.max()) >= self.codec.quan_scale:
+            raise ValueError("symbols out of range [0, quan_scale)")
+        d_sym = self._buf("symbols", s.nbytes)
+        d_sym.upload(s)
+        d_out = self._buf("image_out", H * W * 3)
+        self.decode_image_device(d_sym, H, W, d_out, post_filter)
+        self.synchronize()
+        return d_out.download((H, W, 3), np.uint8)
+
+    def close(self) -> None:
+        for b in self._bufs.values():
+            b.free()
+        self._bufs.clear()
+
+
+def symbol_histogram(codec: Codec, d_sym: DeviceBuffer, n_symbols: int, Q: int,
+                     d_counts: DeviceBuffer | None = None, reset: bool = True) -> np.ndarray:
+    """np.histogram(symbols, range(Q + 1))[0] on the GPU (get_encoded_distribution.py:113-126)."""
+    own = d_counts is None
+    if own:
+        d_counts = codec.alloc(8 * Q)
+    if reset:
+        codec.memset_device(d_counts, 0, 8 * Q)
+    codec.histogram_device(d_sym, n_symbols, Q, d_counts)
+    counts = d_counts.download((Q,), np.uint64)
+    if own:
+        d_counts.free()
+    return counts
