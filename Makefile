@@ -7,7 +7,8 @@ BUILD    := build
 LIB      := tf_image_compression_amd/libtic.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)
 KERNELS  := conv_s1 conv_s2 conv_t2 conv_rgb image_ops
-OBJS     := $(addprefix $(BUILD)/,$(addsuffix .o,$(KERNELS))) $(BUILD)/tic_runtime.o $(BUILD)/range_coder.o
+OBJS     := $(addprefix $(BUILD)/,$(addsuffix .o,$(KERNELS))) $(BUILD)/tic_runtime.o $(BUILD)/range_coder.o \
+            $(BUILD)/host_util.o
 HDRS     := $(wildcard $(CSRC)/*.h) include/tic.h
 
 all: $(LIB)
@@ -19,6 +20,9 @@ $(BUILD)/tic_runtime.o: $(CSRC)/tic_runtime.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(BUILD)/range_coder.o: $(CSRC)/range_coder.cpp include/tic.h | $(BUILD)
+	g++ -O2 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
+
+$(BUILD)/host_util.o: $(CSRC)/host_util.cpp include/tic.h | $(BUILD)
 	g++ -O2 -std=c++17 -fPIC -Wall -Iinclude -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -101,6 +101,8 @@ def uncompress(model, args):
     if args.rmbe:
         from tf_image_compression_amd.rmbe import RmbeFilter
         post = RmbeFilter.from_files(args.rmbe, args.rmbe_norm, device=codec.device)
+    from tf_image_compression_amd.image_codec import ImageCodec
+    ic = ImageCodec(codec, post.codec if post is not None else None)
     out_dir = args.output_dir.format(args.model_num)
     os.makedirs(out_dir, exist_ok=True)
     t0 = time.time()
@@ -115,13 +117,8 @@ def uncompress(model, args):
         else:
             seq = apply_range_decoder(seq_len, path, cum_freq)
         symbols = seq.astype(np.uint8).reshape(-1, eh, ew, ec)       # decode.py:204-208
-        if post is None:
-            rgb = codec.decode(symbols)                                 # np.around fused
-            recons = utils.concat_patches(rgb, height, width, P)
-        else:
-            _, f = codec.decode(symbols, return_float=True)
-            recons = post.apply(utils.concat_patches(f, height, width, P))
-            recons = np.around(recons).astype(np.uint8)                 # submit/2/decoder.py:200
+        # decode -> concat_patches -> (rmbe) -> np.around, all on the GPU
+        recons = ic.decode_image(symbols, height, width, post_filter=post is not None)
         out_path = get_recons_image_path(filename, args, config)
         print(f"recons_image_path: {out_path}")
         utils.imsave(out_path, recons)

@@ -6,9 +6,10 @@ uint8 symbols (patch-major, then h, w, C) -> range coder -> ``.encoded`` files n
 
 Reference: /root/reference/encode.py:17-73 (flags), :76-97 (range coding), :125-212
 (compress).  Differences: ``-g`` picks a HIP device (0..7) instead of setting
-CUDA_VISIBLE_DEVICES; ``-p`` names an .npz of the TF variables (a TF checkpoint reader is
-not part of this build); all patches of an image go through the GPU in one call instead
-of ``sess.run`` batches of 64.  Extra optional flags: ``--norm`` (channel statistics
+CUDA_VISIBLE_DEVICES; ``-p`` names the TF checkpoint prefix (read by tf_checkpoint.py) or an
+.npz of the same variables; the image is uploaded once and reflect-tiled on the GPU
+(image_codec.py), and all its patches go through the encoder in one call instead of
+``sess.run`` batches of 64.  Extra optional flags: ``--norm`` (channel statistics
 npz), ``--dist`` (symbol distribution npy), ``--synthetic-weights`` (seeded weights when
 no checkpoint exists), ``--raw`` (store bit-packed symbols, no entropy coding).
 """
@@ -90,14 +91,15 @@ def compress(model, args):
     print(config)
     P, Q = config["patch_size"], config["quan_scale"]
     codec = model.codec(P, Q)
+    from tf_image_compression_amd.image_codec import ImageCodec
+    ic = ImageCodec(codec)
     cum_freq = None if args.raw else symbol_table(args, config)
     out_dir = args.output_dir.format(args.model_num)
     os.makedirs(out_dir, exist_ok=True)
     t0 = time.time()
     for image_path in utils.read_image_list(args.data_list):
         image = utils.imread(image_path)
-        patches = np.stack(utils.crop_image_input_patches(image, P))
-        symbols = codec.encode(patches)                      # [n, eh, ew, ec] uint8
+        symbols = ic.encode_image(image)                     # [n, eh, ew, ec] uint8
         shape = symbols.shape[1:]
         seq = symbols.reshape(-1)                            # encode.py:175-182 order
         encodepath = get_encodepath(image_path, image, seq.size, args, config, shape)

@@ -197,6 +197,11 @@ int tic_memset_device(tic_handle* h, void* d_ptr, int value, size_t bytes);
  * device): chains a codec handle and an rmbe handle without a host synchronisation. */
 int tic_stream_wait(tic_handle* waiter, tic_handle* signaler);
 
+/* CRC-32C (Castagnoli) of n bytes, continuing `crc` (0 to start).  Host only.  Used by the
+ * TensorFlow checkpoint reader that replaces tf.train.Saver.restore (utils/utils.py:84-93):
+ * table blocks and tensor-bundle entries carry masked CRC-32C checksums. */
+uint32_t tic_crc32c(const void* data, size_t n, uint32_t crc);
+
 /* --- entropy coder (host, no device) ---
  * Replaces the third-party `range_coder` package used by encode.py:86-97 and
  * decode.py:89-99: RangeEncoder(path).encode(data, cum_freq) / .close() and

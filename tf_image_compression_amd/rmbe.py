@@ -5,7 +5,8 @@ network submit/2/rmbe/model.py:113-197), on the gfx950 path.
 filtered and written back, then 128x128 windows at row offset 64 over all full columns;
 edge strips that do not fill a window stay untouched.  The reference rebuilds a TF graph
 and session and restores the weights on every call (run_rmbe_model :28-44); here the
-network lives in one libtic handle and each pass is one batched launch sequence.
+network lives in one libtic handle, the window gather / write-back are kernels
+(image_ops.hip) and each pass is one batched launch sequence (tic_rmbe_image_device).
 """
 from __future__ import annotations
 
@@ -26,26 +27,21 @@ class RmbeFilter:
         import os
         from .weights import load_params, load_normalization
         mean, std = load_normalization(norm_npz if norm_npz and os.path.exists(norm_npz) else None)
-        return cls(load_params(weights_npz), mean, std, device)
-
-    def _pass(self, img, r0, c0, hn, wn):
-        if hn <= 0 or wn <= 0:
-            return img
-        P = PATCH
-        wins = np.stack([img[r0 + i * P:r0 + (i + 1) * P, c0 + j * P:c0 + (j + 1) * P]
-                         for i in range(hn) for j in range(wn)])
-        out = self.codec.rmbe_windows(wins)
-        for i in range(hn):
-            for j in range(wn):
-                img[r0 + i * P:r0 + (i + 1) * P, c0 + j * P:c0 + (j + 1) * P] = out[i * wn + j]
-        return img
+        return cls(load_params(weights_npz, RMBE_ID), mean, std, device)
 
     def apply(self, image):
-        img = np.array(image, dtype=np.float32, copy=True)
+        """rmbe.rmbe(image) (submit/2/rmbe/rmbe.py:15-24): float32 HxWx3 in [0,255] -> filtered
+        copy; both window passes run on the GPU (tic_rmbe_image_device)."""
+        img = np.ascontiguousarray(image, dtype=np.float32)
         h, w, _ = img.shape
-        img = self._pass(img, 0, OFFSET, h // PATCH, (w - OFFSET) // PATCH)      # rmbe_height :70-89
-        img = self._pass(img, OFFSET, 0, (h - OFFSET) // PATCH, w // PATCH)      # rmbe_width :92-111
-        return img
+        d = self.codec.alloc(img.nbytes)
+        try:
+            d.upload(img)
+            self.codec.rmbe_image_device(d, h, w)
+            self.codec.synchronize()
+            return d.download(img.shape, np.float32)
+        finally:
+            d.free()
 
     def close(self):
         self.codec.close()

@@ -38,18 +38,20 @@ def concat_patches(patches, height, width, patch_size):
 
 
 def default_params_file(model_num):
-    """utils/utils.py:86: model_N/params_for_test/params (here + '.npz')."""
+    """utils/utils.py:86: model_N/params_for_test/params (a TF checkpoint prefix, or + '.npz')."""
     return os.path.join(f"model_{model_num}", "params_for_test", "params")
 
 
 def restore_params(args_or_path, model_num=None):
-    """Load weights for a codec: ``args.params_file`` (or the default path) as .npz."""
+    """Load weights for a codec: ``args.params_file`` (or the default path), a TF V2
+    checkpoint prefix (tf_checkpoint.py) or an .npz of the same variable names."""
     from .weights import load_params
     if isinstance(args_or_path, str):
         path = args_or_path
     else:
         path = args_or_path.params_file or default_params_file(args_or_path.model_num)
-    params = load_params(path)
+        model_num = int(args_or_path.model_num)
+    params = load_params(path, model_num)
     print(f"Params in {path} restored complete")
     return params
 

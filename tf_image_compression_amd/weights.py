@@ -48,8 +48,16 @@ def _is_transpose(model_id: int, kernel_name: str) -> bool:
     raise KeyError(kernel_name)
 
 
-def load_params(path: str) -> dict[str, np.ndarray]:
-    """Load an ``.npz`` keyed by TF variable names (no pickle)."""
+def load_params(path: str, model_id: int | None = None) -> dict[str, np.ndarray]:
+    """Load TF-named weights: a TF V2 checkpoint prefix (``<path>.index`` exists — the
+    reference's ``model_N/params_for_test/params``, read by tf_checkpoint.py; with
+    ``model_id`` only that model's variables) or an ``.npz`` keyed by the TF names (no pickle)."""
+    from . import tf_checkpoint
+    if tf_checkpoint.is_checkpoint(path):
+        if model_id is not None:
+            return tf_checkpoint.load_model_params(path, model_id)
+        return {k: np.asarray(v, np.float32) for k, v in tf_checkpoint.read_checkpoint(path).items()
+                if np.asarray(v).dtype.kind == "f"}
     if not path.endswith(".npz"):
         path = path + ".npz"
     with np.load(path, allow_pickle=False) as z:
