@@ -150,12 +150,34 @@ def codec_std():
     return SYNTH_STD
 
 
-def test_last_layer_scatter_form(lib_codec, monkeypatch):
-    """The scatter (col2im) form of the last layer meets the same parity bar."""
-    monkeypatch.setenv("TIC_RGB_OUT_FORM", "scatter")
+@pytest.mark.parametrize("form", ["scatter", "dense"])
+def test_last_layer_mfma_forms(lib_codec, monkeypatch, form):
+    """The MFMA forms of the last layer (col2im, dense sub-pixel) meet the same parity bar
+    as the default VALU form."""
+    monkeypatch.setenv("TIC_RGB_OUT_FORM", form)
     P = 64
     codec, params = lib_codec(0, P)
     _check_codec(codec, params, 0, P, structured_patches(3, P, seed=41))
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 256), (3, 64), (0, 48)])
+def test_last_layer_valu_tilings_bit_identical(lib_codec, monkeypatch, model_id, P):
+    """Every tiling of the VALU last layer (TW 64/32/16, one-shot and persistent; the
+    persistent ones also with a grid capped at 7 so each workgroup walks several tiles) gives
+    identical bytes and floats, including partial edge tiles (P = 48: 24-wide decode_0
+    input) and the unaligned path."""
+    codec, _ = lib_codec(model_id, P)
+    idx = codec.encode(structured_patches(3, P, seed=43))
+    outs = []
+    for t in range(6):
+        monkeypatch.setenv("TIC_RGB_OUT_TILE", str(t))
+        outs.append(codec.decode(idx, return_float=True))
+        if t >= 3:
+            codec.set_option("persist_grid", 7)
+            outs.append(codec.decode(idx, return_float=True))
+            codec.set_option("persist_grid", 0)
+    for u8, f in outs[1:]:
+        assert np.array_equal(u8, outs[0][0]) and np.array_equal(f, outs[0][1])
 
 
 @pytest.mark.parametrize("model_id", [0, 1, 2, 3])

@@ -1,7 +1,10 @@
 // First layer (u8/f32 RGB -> normalise -> stride-2 conv) and last layer
 // (transpose conv -> denormalise -> clip -> round -> u8) of every codec, with their
 // tiling variants (selected per layer by tic_autotune).
+#include <algorithm>
+
 #include "conv3x3.h"
+#include "convT_rgb_valu.h"
 
 namespace tic {
 
@@ -33,9 +36,10 @@ bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream
   return false;
 }
 
-// Variants 0-2: dense sub-pixel form, TH 4/8/16 (one summation order: autotuned).
-// Variants 3-5: scatter form, TH 4/8/16 (different tap summation order; chosen only via
-// TIC_RGB_OUT_FORM=scatter so that tuning never changes results).
+// Last layer: variants 0-2 dense sub-pixel MFMA form (TH 4/8/16), 3-5 scatter MFMA form
+// (TH 4/8/16), 6-11 VALU form (TW 64/32/16; 9-11 persistent, software-pipelined).  The form is a fixed policy (default VALU;
+// TIC_RGB_OUT_FORM=dense|scatter for experiments); tuning picks a tiling within the form,
+// so it never changes results.
 int enc01_variants() { return 2; }  // TH1 = 2, 4
 
 template <int C0, int C1, int TH1>
@@ -62,7 +66,7 @@ bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipS
   return false;
 }
 
-int rgb_out_variants() { return 3; }
+int rgb_out_variants() { return 12; }
 
 template <int CIN, int TH, bool SCATTER>
 static bool rgb_out_th(const RgbOutArgs& a, int n, hipStream_t s) {
@@ -71,6 +75,23 @@ static bool rgb_out_th(const RgbOutArgs& a, int n, hipStream_t s) {
     hipLaunchKernelGGL((convT_rgb_scatter_kernel<CIN, TH>), grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((convT_rgb_kernel<CIN, TH>), grid, dim3(256), 0, s, a);
+  return true;
+}
+
+template <int CIN, int TW>
+static bool rgb_out_valu(const RgbOutArgs& a, int n, hipStream_t s) {
+  dim3 grid((a.W + TW - 1) / TW, (a.H + 256 / TW - 1) / (256 / TW), n);
+  hipLaunchKernelGGL((convT_rgb_valu_kernel<CIN, TW>), grid, dim3(256), 0, s, a);
+  return true;
+}
+
+template <int CIN, int TW>
+static bool rgb_out_valu_persist(const RgbOutArgs& a, int n, hipStream_t s) {
+  const int ntx = (a.W + TW - 1) / TW, nty = (a.H + 256 / TW - 1) / (256 / TW);
+  const int ntiles = ntx * nty * n;
+  int grid = std::min(ntiles, 2 * std::max(1, a.num_cus));
+  if (a.grid_cap > 0) grid = std::min(grid, a.grid_cap);
+  hipLaunchKernelGGL((convT_rgb_valu_persist_kernel<CIN, TW>), dim3(grid), dim3(256), 0, s, a, ntx, nty, ntiles);
   return true;
 }
 
@@ -83,6 +104,12 @@ static bool rgb_out_c(const RgbOutArgs& a, int n, hipStream_t s, int variant) {
     case 3: return rgb_out_th<CIN, 4, true>(a, n, s);
     case 4: return rgb_out_th<CIN, 8, true>(a, n, s);
     case 5: return rgb_out_th<CIN, 16, true>(a, n, s);
+    case 6: return rgb_out_valu<CIN, 64>(a, n, s);
+    case 7: return rgb_out_valu<CIN, 32>(a, n, s);
+    case 8: return rgb_out_valu<CIN, 16>(a, n, s);
+    case 9: return rgb_out_valu_persist<CIN, 64>(a, n, s);
+    case 10: return rgb_out_valu_persist<CIN, 32>(a, n, s);
+    case 11: return rgb_out_valu_persist<CIN, 16>(a, n, s);
   }
   return false;
 }

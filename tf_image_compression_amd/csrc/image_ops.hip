@@ -141,16 +141,23 @@ __global__ void __launch_bounds__(256) sse_u8_kernel(const uint8_t* __restrict__
     const int d = (int)a[nw * 4 + threadIdx.x] - (int)b[nw * 4 + threadIdx.x];
     s += (unsigned long long)(d * d);
   }
-  // wavefront reduction (64 lanes), then one atomic per wave
+  // wavefront reduction (64 lanes), then across the 4 waves in LDS: one atomic per
+  // workgroup (the grid is capped at 2 workgroups per CU, so at most 512 atomics meet)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(acc, s);
+  __shared__ unsigned long long part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(acc, t);
+  }
 }
 
 namespace {
-unsigned grid_for(size_t items, int num_cus) {
+unsigned grid_for(size_t items, int num_cus, int per_cu = 16) {
   const size_t want = (items + 255) / 256;
-  const size_t cap = (size_t)num_cus * 16;  // grid-stride beyond 16 workgroups per CU
+  const size_t cap = (size_t)num_cus * per_cu;  // grid-stride beyond per_cu workgroups per CU
   return (unsigned)std::max<size_t>(1, std::min(want, cap));
 }
 }  // namespace
@@ -179,12 +186,12 @@ void launch_round_u8(const float* in, size_t n, uint8_t* out, int num_cus, hipSt
 }
 
 void launch_histogram(const uint8_t* sym, size_t n, int Q, unsigned long long* counts, int num_cus, hipStream_t s) {
-  hipLaunchKernelGGL(histogram_kernel, dim3(grid_for(n / 4 + 1, num_cus)), dim3(256), 0, s, sym, n, Q, counts);
+  hipLaunchKernelGGL(histogram_kernel, dim3(grid_for(n / 4 + 1, num_cus, 2)), dim3(256), 0, s, sym, n, Q, counts);
 }
 
 void launch_sse_u8(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* acc, int num_cus,
                    hipStream_t s) {
-  hipLaunchKernelGGL(sse_u8_kernel, dim3(grid_for(n / 4 + 1, num_cus)), dim3(256), 0, s, a, b, n, acc);
+  hipLaunchKernelGGL(sse_u8_kernel, dim3(grid_for(n / 4 + 1, num_cus, 2)), dim3(256), 0, s, a, b, n, acc);
 }
 
 }  // namespace tic

@@ -58,11 +58,14 @@ struct RgbOutArgs {
   const float* in;     // [N,H,W,Cin]
   const float* wp;     // dense sub-pixel form: [4 off][Cin/16][16 rows][4][4]
   const float* wp2;    // scatter form: [2 rb][Cin/16][4 g][16 rows][4 t]
+  const float* wraw;   // VALU form: the TF kernel as-is, [3][3][3][Cin]
   const float* bias;   // [3]
   uint8_t* out_u8;     // [N,2H,2W,3] or nullptr
   float* out_f32;      // [N,2H,2W,3] or nullptr
   int H, W;
   float mean[3], std[3];
+  int num_cus;         // persistent variants size their grid from it
+  int grid_cap;        // > 0: cap on the persistent grid (tests force several tiles per workgroup)
 };
 
 typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);
@@ -83,7 +86,10 @@ const ConvEntry* conv_registry_s2(int* count);
 const ConvEntry* conv_registry_t2(int* count);
 
 // First / last layer launchers (conv_rgb.hip); `variant` < rgb_*_variants() selects the
-// tiling / formulation; return false if the width is not compiled.
+// tiling / formulation; return false if the width is not compiled.  Last layer: variants
+// 0-2 dense sub-pixel MFMA form (TH 4/8/16), 3-5 col2im MFMA form (TH 4/8/16), 6-11 VALU
+// form (TW 64/32/16, then the same persistent + software-pipelined); each form has its own summation order, the tilings of one form are
+// bit-identical.
 int rgb_in_variants();
 int enc01_variants();
 bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant);

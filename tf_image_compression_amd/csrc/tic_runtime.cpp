@@ -257,6 +257,7 @@ struct LayerRT {
   bool has_k = false, has_b = false;
   float* d_w = nullptr;
   float* d_w2 = nullptr;  // alternate packing (last layer: scatter form)
+  float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
@@ -382,11 +383,30 @@ int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(i
 }
 
 const int kRgbInDefault = 2;   // TH 16
-const int kRgbOutDefault = 0;  // dense sub-pixel form, TH 4
 
-int rgb_out_forced() {  // TIC_RGB_OUT_FORM=scatter -> scatter form TH 8 (experiments/tests)
+// Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
+// each form has its own summation order.  Default: the VALU form (variants 6-8);
+// TIC_RGB_OUT_FORM=dense (0-2) or scatter (3-5) for experiments and tests.  Tuning and
+// tic_autotune_step choose a tiling inside the form only.
+struct RgbOutForm {
+  int lo, hi;
+  bool has(int v) const { return v >= lo && v < hi; }
+};
+RgbOutForm rgb_out_form() {
   const char* f = getenv("TIC_RGB_OUT_FORM");
-  return (f && std::string(f) == "scatter") ? 4 : -1;
+  const std::string s = f ? f : "";
+  if (s == "dense") return {0, 3};
+  if (s == "scatter") return {3, 6};
+  return {6, 12};
+}
+int rgb_out_variant(const std::map<int, int>& tuned, int n) {
+  const RgbOutForm fm = rgb_out_form();
+  if (const char* t = getenv("TIC_RGB_OUT_TILE")) {  // tests: force tiling t of the form
+    const int v = fm.lo + atoi(t);
+    if (fm.has(v)) return v;
+  }
+  auto it = tuned.find(n);
+  return it != tuned.end() && fm.has(it->second) ? it->second : fm.lo;
 }
 
 struct Prof {
@@ -496,6 +516,9 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.in = src;
       a.wp = lay.d_w;
       a.wp2 = lay.d_w2;
+      a.wraw = lay.d_w3;
+      a.num_cus = h->num_cus;
+      a.grid_cap = h->persist_grid;
       a.bias = lay.d_b;
       a.out_u8 = d_rgb;
       a.out_f32 = d_f32;
@@ -504,15 +527,15 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         a.mean[c] = h->mean[c];
         a.std[c] = h->std[c];
       }
+      const RgbOutForm fm = rgb_out_form();
       auto it = lay.tuned_var.find(n);
-      int var = it != lay.tuned_var.end() ? it->second : kRgbOutDefault;
-      const int forced = rgb_out_forced();
-      if (forced >= 0) var = forced;
-      else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
-        int rc = time_variants(st, tic::rgb_out_variants(), h->tune_reps,
-                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, st, v); }, &var,
+      int var = rgb_out_variant(lay.tuned_var, n);
+      if (h->tune_reps > 0 && (it == lay.tuned_var.end() || !fm.has(it->second)) && !getenv("TIC_RGB_OUT_TILE")) {
+        int rc = time_variants(st, fm.hi - fm.lo, h->tune_reps,
+                               [&](int v) { return tic::launch_rgb_out(d.cin, a, n, st, fm.lo + v); }, &var,
                                "rgb_out", n);
         if (rc) return rc;
+        var += fm.lo;
         lay.tuned_var[n] = var;
       }
       if (!tic::launch_rgb_out(d.cin, a, n, st, var))
@@ -781,6 +804,7 @@ void tic_destroy(tic_handle* h) {
   for (auto& l : h->layers) {
     if (l.d_w) (void)hipFree(l.d_w);
     if (l.d_w2) (void)hipFree(l.d_w2);
+    if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
@@ -867,13 +891,16 @@ int tic_finalize(tic_handle* h) {
     else pack_generic(l.k.data(), l.def.kind, l.def.cin, l.def.cout, &wp);
     if (l.d_w) (void)hipFree(l.d_w);
     if (l.d_w2) (void)hipFree(l.d_w2);
+    if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_b) (void)hipFree(l.d_b);
-    l.d_w = l.d_w2 = l.d_b = nullptr;
+    l.d_w = l.d_w2 = l.d_w3 = l.d_b = nullptr;
     if (i == L - 1) {
       std::vector<float> w2;
       pack_rgb_out_scatter(l.k.data(), l.def.cin, &w2);
       HIP_TRY(hipMalloc((void**)&l.d_w2, w2.size() * sizeof(float)));
       HIP_TRY(hipMemcpy(l.d_w2, w2.data(), w2.size() * sizeof(float), hipMemcpyHostToDevice));
+      HIP_TRY(hipMalloc((void**)&l.d_w3, l.k.size() * sizeof(float)));
+      HIP_TRY(hipMemcpy(l.d_w3, l.k.data(), l.k.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMalloc((void**)&l.d_w, wp.size() * sizeof(float)));
     HIP_TRY(hipMemcpy(l.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -1247,13 +1274,12 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       const LayerDef& d = l.def;
       const bool first = i == 0, last = i == L - 1;
       if ((first || i == 1) && fuses01(h)) continue;
-      if (last && rgb_out_forced() >= 0) continue;
       if (first || last) {
-        const int nv = first ? tic::rgb_in_variants() : tic::rgb_out_variants();
-        const int keep = l.tuned_var[sizes[0]];
+        const RgbOutForm fm = first ? RgbOutForm{0, tic::rgb_in_variants()} : rgb_out_form();
+        const int keep = first ? l.tuned_var[sizes[0]] : rgb_out_variant(l.tuned_var, sizes[0]);
         int best_v = keep;
         float best = cur;
-        for (int v = 0; v < nv && !rc; ++v) {
+        for (int v = fm.lo; v < fm.hi && !rc; ++v) {
           if (v == keep) continue;
           for (int m : sizes) l.tuned_var[m] = v;
           float ms = 0.f;
@@ -1311,10 +1337,10 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
   const int L = (int)h->layers.size();
   if (i == 0 || i == L - 1) {
     auto iv = l.tuned_var.find(n);
-    const int v = iv != l.tuned_var.end() ? iv->second : (i == 0 ? kRgbInDefault : kRgbOutDefault);
-    static const int th_in[3] = {4, 8, 16}, th_out[6] = {4, 8, 16, 4, 8, 16};
+    const int v = i == 0 ? (iv != l.tuned_var.end() ? iv->second : kRgbInDefault) : rgb_out_variant(l.tuned_var, n);
+    static const int th_in[3] = {4, 8, 16}, th_out[12] = {4, 8, 16, 4, 8, 16, 4, 8, 16, 4, 8, 16};
     *th = i == 0 ? th_in[v] : th_out[v];
-    *nsplit = (i == L - 1 && v >= 3) ? 1 : 0;  // last layer: 1 = scatter form
+    *nsplit = i == L - 1 ? v / 3 : 0;  // last layer: 0 dense, 1 scatter, 2 VALU, 3 VALU persistent
     return TIC_OK;
   }
   auto it = l.tuned.find(n);
@@ -1352,10 +1378,13 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     }
   } else if (i == 0 || i == L - 1) {
     auto iv = l.tuned_var.find(n);
-    const int v = iv != l.tuned_var.end() ? iv->second : (i == 0 ? kRgbInDefault : kRgbOutDefault);
-    static const int th[3] = {4, 8, 16};
+    const int v = i == 0 ? (iv != l.tuned_var.end() ? iv->second : kRgbInDefault) : rgb_out_variant(l.tuned_var, n);
+    static const int th[3] = {4, 8, 16}, tw[3] = {64, 32, 16};
     if (i == 0)
       snprintf(buf, sizeof buf, "conv_rgb_s2_kernel<%d,%d,%s>", d.cout, th[v % 3], tf[!h->rmbe()]);
+    else if (v >= 6)
+      snprintf(buf, sizeof buf, "%s<%d,%d>", v >= 9 ? "convT_rgb_valu_persist_kernel" : "convT_rgb_valu_kernel", d.cin,
+               tw[v % 3]);
     else
       snprintf(buf, sizeof buf, "%s<%d,%d>", v >= 3 ? "convT_rgb_scatter_kernel" : "convT_rgb_kernel", d.cin,
                th[v % 3]);
