@@ -150,6 +150,66 @@ def codec_std():
     return SYNTH_STD
 
 
+# Winograd F(2x2,3x3) tilings of the stride-1 layers: (th = 2 TTY, nsplit, NN)
+WINO_TILES = [(2, 1, 1), (4, 1, 1), (4, 2, 1), (4, 4, 1), (2, 4, 1), (4, 1, 2), (8, 1, 2)]
+
+
+@pytest.mark.parametrize("act,res,H,W", [(1, False, 16, 16), (1, True, 20, 13), (0, False, 33, 17),
+                                         (1, True, 64, 64), (1, False, 7, 40)])
+def test_conv3x3_winograd(lib_codec, act, res, H, W):
+    """Winograd form of the stride-1 layers: within the per-layer bar of the oracle (same
+    3e-5 relative bound as the direct form), every Winograd tiling bit-identical to every
+    other, partial tiles at odd sizes included."""
+    import os
+    codec, _ = lib_codec(0, 64)
+    cin = cout = 64
+    r = np.random.default_rng(np.random.PCG64(777 + H * 100 + W))
+    n = 2
+    x = r.standard_normal((n, H, W, cin)).astype(np.float32)
+    k = (r.standard_normal((3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    b = (r.standard_normal(cout) * 0.1).astype(np.float32)
+    ref = o.my_conv2d(x, {"l/kernel": k, "l/bias": b}, "l", 1, "relu" if act else "identity")
+    resid = r.standard_normal(ref.shape).astype(np.float32) if res else None
+    if res:
+        ref = ref + resid
+    d_in, d_out = codec.alloc(x.nbytes), codec.alloc(ref.nbytes)
+    d_in.upload(x)
+    d_res = None
+    if res:
+        d_res = codec.alloc(resid.nbytes)
+        d_res.upload(resid)
+    outs = []
+    try:
+        for th, ns, nn in WINO_TILES:
+            os.environ["TIC_FORCE_TILE"] = f"{th},{ns},4,{nn}"
+            d_out.upload(np.full(ref.shape, np.nan, np.float32))
+            codec.conv3x3_device(0, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
+            outs.append(((th, ns, nn), d_out.download(ref.shape, np.float32)))
+    finally:
+        os.environ.pop("TIC_FORCE_TILE", None)
+    for buf in (d_in, d_out, d_res):
+        if buf is not None:
+            buf.free()
+    scale = max(1.0, float(np.max(np.abs(ref))))
+    for tile, got in outs:
+        err = float(np.max(np.abs(got - ref)))
+        assert err <= 3e-5 * scale, (tile, err, scale)
+        assert np.array_equal(got, outs[0][1]), tile
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 64), (3, 64), (1, 32)])
+def test_codec_s1_forms(lib_codec, model_id, P):
+    """Both stride-1 forms (direct, Winograd) meet the end-to-end parity bar."""
+    codec, params = lib_codec(model_id, P)
+    patches = structured_patches(2, P, seed=61 + model_id)
+    try:
+        for form in (0, 1):
+            codec.set_option("s1_form", form)
+            _check_codec(codec, params, model_id, P, patches)
+    finally:
+        codec.set_option("s1_form", -1)
+
+
 @pytest.mark.parametrize("form", ["scatter", "dense"])
 def test_last_layer_mfma_forms(lib_codec, monkeypatch, form):
     """The MFMA forms of the last layer (col2im, dense sub-pixel) meet the same parity bar

@@ -6,24 +6,144 @@
 // channels = 12 outputs from 9 (phase, input offset) pairs x Cin products = 864 MACs at
 // Cin = 32.  Every MFMA formulation pads that badly — the dense sub-pixel GEMM
 // (convT_rgb_kernel) spends 2048 MAC slots per position (42 % useful: 3 of 4 rows, 9 of
-// 16 (phase, offset) blocks), the col2im form needs an LDS reduction pass — while a
-// v_fma_f32 with the weight in an SGPR retires 64 useful MACs per 2 cycles per SIMD, the
-// same 64 FLOP/clk/SIMD as the fp32 MFMA.  At 100 % useful work the layer's arithmetic
-// (9 x Cin x 3 x 2 FLOP per input position) is well under its HBM time (Cin x 4 bytes in,
-// 12 bytes out per position), so the kernel is built to stream: one input position per
-// thread, its 2x2 output pixels staged in LDS and written back as 16-byte row chunks.
+// 16 (phase, offset) blocks), the col2im form needs an LDS reduction pass — while a wave64
+// v_fma_f32 with a wave-uniform weight retires 64 useful MACs per 2 cycles per SIMD, the
+// f32 MFMA rate.  At 100 % useful work the layer's arithmetic (9 x Cin x 3 x 2 FLOP per
+// input position) is of the order of its HBM time (Cin x 4 bytes in, 12 bytes out per
+// position), so the kernel is built to stream: one input position per thread, its 2x2
+// output pixels staged in LDS and written back as 16-byte row chunks.
 //
 // Workgroup: TH x TW input positions (TH * TW = 256, one per thread) + one halo row / column
 // above / left (input offsets d in {0,-1}: T(0) = {(k=0,d=0), (k=2,d=-1)}, T(1) = {(k=1,d=0)}),
 // staged in LDS with pixel stride Cin + 4 floats (== 4 mod 8: the ds_read_b128 of 16
 // consecutive positions hits 16 distinct bank slots).  Weights: the TF kernel as-is,
-// [3 ky][3 kx][3 co][Cin] float32, read with wave-uniform addresses (scalar loads).
+// [3 ky][3 kx][3 co][Cin] float32; the one-shot kernel reads them with wave-uniform
+// addresses (scalar loads; many workgroups per CU hide their latency), the persistent one
+// stages them once per workgroup in LDS and reads them as broadcast ds_read_b128 (scalar
+// loads there share lgkmcnt with the tile's LDS reads and serialise the loop).
 // Summation order per output: input offsets (0,0), (0,-1), (-1,0), (-1,-1), Cin ascending
-// within each — the same for every TW, so every tiling is bit-identical.
+// within each — the same for every TW and both kernels, so every tiling is bit-identical.
+// The helpers below are shared with the fused decoder tail.
 #pragma once
 #include "conv3x3.h"
 
 namespace tic {
+
+// acc[phase][co] += the 9 (phase, offset) products of one input position.  `self` points at
+// the position in an LDS tile of pitch PS floats per position and LC positions per row, so
+// that offset (-1, 0) is self - LC*PS and (0, -1) is self - PS.  `w` is [3][3][3][CIN].
+template <int CIN, int PS, int LC>
+__device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, float (&acc)[4][3]) {
+  constexpr int C4 = CIN / 4;
+#pragma unroll
+  for (int off = 0; off < 4; ++off) {
+    const int dy = -(off >> 1), dx = -(off & 1);
+    const float* src = self + (dy * LC + dx) * PS;
+    float x[CIN];
+#pragma unroll
+    for (int c4 = 0; c4 < C4; ++c4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * c4);
+      x[4 * c4] = v.x;
+      x[4 * c4 + 1] = v.y;
+      x[4 * c4 + 2] = v.z;
+      x[4 * c4 + 3] = v.w;
+    }
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+      if ((dy != 0 && py == 1) || (dx != 0 && px == 1)) continue;  // phase does not use this offset
+      const int ky = py ? 1 : (dy == 0 ? 0 : 2);
+      const int kx = px ? 1 : (dx == 0 ? 0 : 2);
+#pragma unroll
+      for (int co = 0; co < 3; ++co) {
+        const float* wk = w + ((ky * 3 + kx) * 3 + co) * CIN;
+#pragma unroll
+        for (int c4 = 0; c4 < C4; ++c4) {
+          const f32x4 wv = *reinterpret_cast<const f32x4*>(wk + 4 * c4);
+          acc[ph][co] = fmaf(x[4 * c4], wv.x, acc[ph][co]);
+          acc[ph][co] = fmaf(x[4 * c4 + 1], wv.y, acc[ph][co]);
+          acc[ph][co] = fmaf(x[4 * c4 + 2], wv.z, acc[ph][co]);
+          acc[ph][co] = fmaf(x[4 * c4 + 3], wv.w, acc[ph][co]);
+        }
+      }
+    }
+  }
+}
+
+// + bias, * std + mean, clip -> LDS output tile row-major [.][OW] f32 at output pixel
+// (2r + py, 2c + px).
+__device__ __forceinline__ void rgb_out_epilogue(const RgbOutArgs& a, const float (&acc)[4][3], float* lout,
+                                                 int OW, int r, int c) {
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    const int py = ph >> 1, px = ph & 1;
+#pragma unroll
+    for (int co = 0; co < 3; ++co) {
+      const float v = __fadd_rn(acc[ph][co], a.bias[co]);
+      float d = __fadd_rn(__fmul_rn(v, a.std[co]), a.mean[co]);
+      d = fminf(fmaxf(d, 0.f), 255.f);
+      lout[(2 * r + py) * OW + (2 * c + px) * 3 + co] = d;
+    }
+  }
+}
+
+// Write the staged output tile (2TH x 2TW pixels at input origin (gy0, gx0) of image nimg):
+// whole 16-byte row chunks when the tile is interior and aligned, else element-wise.
+template <int TH, int TW, int NT>
+__device__ __forceinline__ void rgb_out_store(const RgbOutArgs& a, const float* lout, int tid, int gy0, int gx0,
+                                              int nimg) {
+  constexpr int OW = 2 * TW * 3;  // floats per output tile row
+  const int Ho = 2 * a.H, Wo = 2 * a.W;
+  const int oy0 = 2 * gy0, ox0 = 2 * gx0;
+  const int rows = min(2 * TH, Ho - oy0), cols = min(2 * TW, Wo - ox0);
+  const size_t row_base = ((size_t)nimg * Ho + oy0) * Wo + ox0;  // pixel index of the tile origin
+  const bool full = cols == 2 * TW;
+  if (a.out_u8) {
+    const bool vec = full && ((Wo * 3) % 16 == 0) && ((ox0 * 3) % 16 == 0) && ((uintptr_t)a.out_u8 % 16 == 0);
+    if (vec) {
+      constexpr int CH = OW / 16;  // 16-byte chunks per tile row (OW u8 bytes)
+      for (int e = tid; e < rows * CH; e += NT) {
+        const int rr = e / CH, ch = e % CH;
+        const float* s = &lout[rr * OW + ch * 16];
+        uint32_t wv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          wv[k] = (uint32_t)rintf(s[4 * k]) | ((uint32_t)rintf(s[4 * k + 1]) << 8) |
+                  ((uint32_t)rintf(s[4 * k + 2]) << 16) | ((uint32_t)rintf(s[4 * k + 3]) << 24);
+        *reinterpret_cast<uint4*>(a.out_u8 + (row_base + (size_t)rr * Wo) * 3 + ch * 16) =
+            make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+    } else {
+      for (int e = tid; e < rows * cols * 3; e += NT) {
+        const int rr = e / (cols * 3), k = e % (cols * 3);
+        a.out_u8[(row_base + (size_t)rr * Wo) * 3 + k] = (uint8_t)rintf(lout[rr * OW + k]);
+      }
+    }
+  }
+  if (a.out_f32) {
+    const bool vec = full && ((Wo * 3) % 4 == 0) && ((ox0 * 3) % 4 == 0) && ((uintptr_t)a.out_f32 % 16 == 0);
+    if (vec) {
+      constexpr int CH = OW / 4;  // 16-byte chunks per tile row (OW floats)
+      for (int e = tid; e < rows * CH; e += NT) {
+        const int rr = e / CH, ch = e % CH;
+        *reinterpret_cast<f32x4*>(a.out_f32 + (row_base + (size_t)rr * Wo) * 3 + ch * 4) =
+            *reinterpret_cast<const f32x4*>(&lout[rr * OW + ch * 4]);
+      }
+    } else {
+      for (int e = tid; e < rows * cols * 3; e += NT) {
+        const int rr = e / (cols * 3), k = e % (cols * 3);
+        a.out_f32[(row_base + (size_t)rr * Wo) * 3 + k] = lout[rr * OW + k];
+      }
+    }
+  }
+}
+
+// The raw [3][3][3][CIN] kernel into LDS (16-byte aligned source: a device allocation).
+template <int CIN, int NT>
+__device__ __forceinline__ void rgb_out_load_weights(const float* __restrict__ wraw, float* wsh, int tid) {
+  for (int e = tid; e < 27 * CIN / 4; e += NT)
+    reinterpret_cast<f32x4*>(wsh)[e] = reinterpret_cast<const f32x4*>(wraw)[e];
+}
 
 template <int CIN, int TW>
 __global__ void __launch_bounds__(256) convT_rgb_valu_kernel(const RgbOutArgs a) {
@@ -39,7 +159,6 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_kernel(const RgbOutArgs a)
   const int gx0 = blockIdx.x * TW, gy0 = blockIdx.y * TH, nimg = blockIdx.z;
   const int H = a.H, W = a.W;
   const float* __restrict__ in = a.in;
-  const float* __restrict__ w = a.wraw;  // raw TF layout [3][3][3][CIN]
 
   // ---- stage input positions (gy0-1 .. gy0+TH-1) x (gx0-1 .. gx0+TW-1), zero outside ----
   constexpr int NSTAGE = LR * LC * C4;
@@ -68,101 +187,13 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_kernel(const RgbOutArgs a)
   }
   __syncthreads();
 
-  // ---- 864 (Cin = 32) fmas per position, weights uniform across the wave ----
   const int r = tid / TW, c = tid % TW;
-  float acc[4][3];
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int co = 0; co < 3; ++co) acc[p][co] = 0.f;
-#pragma unroll
-  for (int off = 0; off < 4; ++off) {
-    const int dy = -(off >> 1), dx = -(off & 1);
-    const float* src = &lds[((r + 1 + dy) * LC + (c + 1 + dx)) * PS];
-    float x[CIN];
-#pragma unroll
-    for (int c4 = 0; c4 < C4; ++c4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * c4);
-      x[4 * c4] = v.x;
-      x[4 * c4 + 1] = v.y;
-      x[4 * c4 + 2] = v.z;
-      x[4 * c4 + 3] = v.w;
-    }
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      const int py = ph >> 1, px = ph & 1;
-      if ((dy != 0 && py == 1) || (dx != 0 && px == 1)) continue;  // phase does not use this offset
-      const int ky = py ? 1 : (dy == 0 ? 0 : 2);
-      const int kx = px ? 1 : (dx == 0 ? 0 : 2);
-#pragma unroll
-      for (int co = 0; co < 3; ++co) {
-        const float* wk = w + ((ky * 3 + kx) * 3 + co) * CIN;
-#pragma unroll
-        for (int ci = 0; ci < CIN; ++ci) acc[ph][co] = fmaf(x[ci], wk[ci], acc[ph][co]);
-      }
-    }
-  }
+  float acc[4][3] = {};
+  rgb_out_fma<CIN, PS, LC>(&lds[((r + 1) * LC + (c + 1)) * PS], a.wraw, acc);
   __syncthreads();  // input tile no longer needed: reuse LDS for the output tile
-
-  // ---- epilogue: + bias, * std + mean, clip -> LDS output tile [2TH][2TW][3] f32 ----
-  constexpr int OW = 2 * TW * 3;  // floats per output tile row
-#pragma unroll
-  for (int ph = 0; ph < 4; ++ph) {
-    const int py = ph >> 1, px = ph & 1;
-#pragma unroll
-    for (int co = 0; co < 3; ++co) {
-      const float v = __fadd_rn(acc[ph][co], a.bias[co]);
-      float d = __fadd_rn(__fmul_rn(v, a.std[co]), a.mean[co]);
-      d = fminf(fmaxf(d, 0.f), 255.f);
-      lds[(2 * r + py) * OW + (2 * c + px) * 3 + co] = d;
-    }
-  }
+  rgb_out_epilogue(a, acc, lds, 2 * TW * 3, r, c);
   __syncthreads();
-
-  // ---- write-back: whole 16-byte row chunks when the tile is interior and aligned ----
-  const int Ho = 2 * H, Wo = 2 * W;
-  const int oy0 = 2 * gy0, ox0 = 2 * gx0;
-  const int rows = min(2 * TH, Ho - oy0), cols = min(2 * TW, Wo - ox0);
-  const size_t row_base = ((size_t)nimg * Ho + oy0) * Wo + ox0;  // pixel index of the tile origin
-  const bool full = cols == 2 * TW;
-  if (a.out_u8) {
-    const bool vec = full && ((Wo * 3) % 16 == 0) && ((ox0 * 3) % 16 == 0) && ((uintptr_t)a.out_u8 % 16 == 0);
-    if (vec) {
-      constexpr int CH = OW / 16;  // 16-byte chunks per tile row (OW u8 bytes)
-      for (int e = tid; e < rows * CH; e += 256) {
-        const int rr = e / CH, ch = e % CH;
-        const float* s = &lds[rr * OW + ch * 16];
-        uint32_t wv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          wv[k] = (uint32_t)rintf(s[4 * k]) | ((uint32_t)rintf(s[4 * k + 1]) << 8) |
-                  ((uint32_t)rintf(s[4 * k + 2]) << 16) | ((uint32_t)rintf(s[4 * k + 3]) << 24);
-        uint8_t* dst = a.out_u8 + (row_base + (size_t)rr * Wo) * 3 + ch * 16;
-        *reinterpret_cast<uint4*>(dst) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-      }
-    } else {
-      for (int e = tid; e < rows * cols * 3; e += 256) {
-        const int rr = e / (cols * 3), k = e % (cols * 3);
-        a.out_u8[(row_base + (size_t)rr * Wo) * 3 + k] = (uint8_t)rintf(lds[rr * OW + k]);
-      }
-    }
-  }
-  if (a.out_f32) {
-    const bool vec = full && ((Wo * 3) % 4 == 0) && ((ox0 * 3) % 4 == 0) && ((uintptr_t)a.out_f32 % 16 == 0);
-    if (vec) {
-      constexpr int CH = OW / 4;  // 16-byte chunks per tile row (OW floats)
-      for (int e = tid; e < rows * CH; e += 256) {
-        const int rr = e / CH, ch = e % CH;
-        *reinterpret_cast<f32x4*>(a.out_f32 + (row_base + (size_t)rr * Wo) * 3 + ch * 4) =
-            *reinterpret_cast<const f32x4*>(&lds[rr * OW + ch * 4]);
-      }
-    } else {
-      for (int e = tid; e < rows * cols * 3; e += 256) {
-        const int rr = e / (cols * 3), k = e % (cols * 3);
-        a.out_f32[(row_base + (size_t)rr * Wo) * 3 + k] = lds[rr * OW + k];
-      }
-    }
-  }
+  rgb_out_store<TH, TW, 256>(a, lds, tid, gy0, gx0, nimg);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -170,8 +201,9 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_kernel(const RgbOutArgs a)
 // tiles t, t + grid, ...  The global loads of the NEXT tile are issued into registers
 // right after this tile's inputs land in LDS, so they fly while this tile computes and
 // writes back (the one-shot kernel's workgroups all load, then all compute, then all
-// store in lock-step, which leaves HBM idle half the time).  Same arithmetic, same
-// order: bit-identical to convT_rgb_valu_kernel.
+// store in lock-step, which leaves HBM idle half the time).  Weights sit in LDS for the
+// workgroup's lifetime.  Same arithmetic, same order: bit-identical to
+// convT_rgb_valu_kernel.
 // ---------------------------------------------------------------------------------------
 template <int CIN, int TW>
 __global__ void __launch_bounds__(256) convT_rgb_valu_persist_kernel(const RgbOutArgs a, int ntx, int nty,
@@ -184,14 +216,14 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_persist_kernel(const RgbOu
   constexpr int OUT_FLOATS = 2 * TH * OW;
   constexpr int NSTAGE = LR * LC * C4;
   constexpr int NIT = (NSTAGE + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float smem[IN_FLOATS + OUT_FLOATS];
+  __shared__ __attribute__((aligned(16))) float smem[IN_FLOATS + OUT_FLOATS + 27 * CIN];
   float* const lin = smem;
   float* const lout = smem + IN_FLOATS;
+  float* const wsh = smem + IN_FLOATS + OUT_FLOATS;
 
   const int tid = threadIdx.x;
-  const int H = a.H, W = a.W, Ho = 2 * H, Wo = 2 * W;
+  const int H = a.H, W = a.W;
   const float* __restrict__ in = a.in;
-  const float* __restrict__ w = a.wraw;
   const int r = tid / TW, c = tid % TW;
 
   f32x4 pre[NIT];
@@ -213,6 +245,7 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_persist_kernel(const RgbOu
   int t = blockIdx.x;
   if (t >= ntiles) return;
   issue(t);
+  rgb_out_load_weights<CIN, 256>(a.wraw, wsh, tid);
   for (; t < ntiles; t += gridDim.x) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
@@ -222,94 +255,13 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_persist_kernel(const RgbOu
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) issue(t + gridDim.x);
 
-    float acc[4][3];
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int co = 0; co < 3; ++co) acc[p][co] = 0.f;
-#pragma unroll
-    for (int off = 0; off < 4; ++off) {
-      const int dy = -(off >> 1), dx = -(off & 1);
-      const float* src = &lin[((r + 1 + dy) * LC + (c + 1 + dx)) * PS];
-      float x[CIN];
-#pragma unroll
-      for (int c4 = 0; c4 < C4; ++c4) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * c4);
-        x[4 * c4] = v.x;
-        x[4 * c4 + 1] = v.y;
-        x[4 * c4 + 2] = v.z;
-        x[4 * c4 + 3] = v.w;
-      }
-#pragma unroll
-      for (int ph = 0; ph < 4; ++ph) {
-        const int py = ph >> 1, px = ph & 1;
-        if ((dy != 0 && py == 1) || (dx != 0 && px == 1)) continue;
-        const int ky = py ? 1 : (dy == 0 ? 0 : 2);
-        const int kx = px ? 1 : (dx == 0 ? 0 : 2);
-#pragma unroll
-        for (int co = 0; co < 3; ++co) {
-          const float* wk = w + ((ky * 3 + kx) * 3 + co) * CIN;
-#pragma unroll
-          for (int ci = 0; ci < CIN; ++ci) acc[ph][co] = fmaf(x[ci], wk[ci], acc[ph][co]);
-        }
-      }
-    }
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      const int py = ph >> 1, px = ph & 1;
-#pragma unroll
-      for (int co = 0; co < 3; ++co) {
-        const float v = __fadd_rn(acc[ph][co], a.bias[co]);
-        float d = __fadd_rn(__fmul_rn(v, a.std[co]), a.mean[co]);
-        d = fminf(fmaxf(d, 0.f), 255.f);
-        lout[(2 * r + py) * OW + (2 * c + px) * 3 + co] = d;
-      }
-    }
+    float acc[4][3] = {};
+    rgb_out_fma<CIN, PS, LC>(&lin[((r + 1) * LC + (c + 1)) * PS], wsh, acc);
+    rgb_out_epilogue(a, acc, lout, OW, r, c);
     __syncthreads();
 
     const int gx0 = (t % ntx) * TW, gy0 = ((t / ntx) % nty) * TH, nimg = t / (ntx * nty);
-    const int oy0 = 2 * gy0, ox0 = 2 * gx0;
-    const int rows = min(2 * TH, Ho - oy0), cols = min(2 * TW, Wo - ox0);
-    const size_t row_base = ((size_t)nimg * Ho + oy0) * Wo + ox0;
-    const bool full = cols == 2 * TW;
-    if (a.out_u8) {
-      const bool vec = full && ((Wo * 3) % 16 == 0) && ((ox0 * 3) % 16 == 0) && ((uintptr_t)a.out_u8 % 16 == 0);
-      if (vec) {
-        constexpr int CH = OW / 16;
-        for (int e = tid; e < rows * CH; e += 256) {
-          const int rr = e / CH, ch = e % CH;
-          const float* s = &lout[rr * OW + ch * 16];
-          uint32_t wv[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            wv[k] = (uint32_t)rintf(s[4 * k]) | ((uint32_t)rintf(s[4 * k + 1]) << 8) |
-                    ((uint32_t)rintf(s[4 * k + 2]) << 16) | ((uint32_t)rintf(s[4 * k + 3]) << 24);
-          *reinterpret_cast<uint4*>(a.out_u8 + (row_base + (size_t)rr * Wo) * 3 + ch * 16) =
-              make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        }
-      } else {
-        for (int e = tid; e < rows * cols * 3; e += 256) {
-          const int rr = e / (cols * 3), k = e % (cols * 3);
-          a.out_u8[(row_base + (size_t)rr * Wo) * 3 + k] = (uint8_t)rintf(lout[rr * OW + k]);
-        }
-      }
-    }
-    if (a.out_f32) {
-      const bool vec = full && ((Wo * 3) % 4 == 0) && ((ox0 * 3) % 4 == 0) && ((uintptr_t)a.out_f32 % 16 == 0);
-      if (vec) {
-        constexpr int CH = OW / 4;
-        for (int e = tid; e < rows * CH; e += 256) {
-          const int rr = e / CH, ch = e % CH;
-          *reinterpret_cast<f32x4*>(a.out_f32 + (row_base + (size_t)rr * Wo) * 3 + ch * 4) =
-              *reinterpret_cast<const f32x4*>(&lout[rr * OW + ch * 4]);
-        }
-      } else {
-        for (int e = tid; e < rows * cols * 3; e += 256) {
-          const int rr = e / (cols * 3), k = e % (cols * 3);
-          a.out_f32[(row_base + (size_t)rr * Wo) * 3 + k] = lout[rr * OW + k];
-        }
-      }
-    }
+    rgb_out_store<TH, TW, 256>(a, lout, tid, gy0, gx0, nimg);
   }
 }
 

@@ -1,6 +1,9 @@
 // Stride-1 'SAME' 3x3 convolutions: res_block convs (basic_block/basic_block.py:74-93),
 // encode_4 / decode_4 of model_0/1 (model_0/model.py:124-134,159-169), rmbe conv_3/4.
-// Several tilings per layer type; the runtime picks by grid size (tic_runtime.cpp).
+// Two forms: the direct implicit GEMM (conv3x3_kernel, several tilings) and Winograd
+// F(2x2,3x3) (conv3x3_wino.h, weight source 4); the runtime picks the form by policy
+// (option "s1_form") and a tiling within it by grid size or measurement (tic_runtime.cpp).
+#include "conv3x3_wino.h"
 #include "conv_launch.h"
 
 #define S1_VARIANTS(ACT, RES, IN, OUT)                                 \
@@ -12,6 +15,17 @@
       TIC_CONV3(MODE_S1, 64, 64, 4, 4, 4, ACT, RES, IN, OUT),          \
       TIC_CONV3(MODE_S1, 64, 64, 1, 1, 1, ACT, RES, IN, OUT)
 
+// Winograd tilings (TTY, NN, NSPLIT): 2x32, 4x16 output pixels per 16-tile block; the
+// channel splits give the 16x16 bottleneck layers of model_0/1 enough workgroups.
+#define S1_WINO(ACT, RES, IN, OUT)                          \
+  TIC_WINO(64, 64, 1, 1, 1, ACT, RES, IN, OUT),             \
+      TIC_WINO(64, 64, 2, 1, 1, ACT, RES, IN, OUT),         \
+      TIC_WINO(64, 64, 2, 1, 2, ACT, RES, IN, OUT),         \
+      TIC_WINO(64, 64, 2, 1, 4, ACT, RES, IN, OUT),         \
+      TIC_WINO(64, 64, 1, 1, 4, ACT, RES, IN, OUT),         \
+      TIC_WINO(64, 64, 2, 2, 1, ACT, RES, IN, OUT),         \
+      TIC_WINO(64, 64, 4, 2, 1, ACT, RES, IN, OUT)
+
 namespace tic {
 static const ConvEntry kS1[] = {
     S1_VARIANTS(ACT_RELU, false, IN_F32, OUT_F32),
@@ -19,6 +33,11 @@ static const ConvEntry kS1[] = {
     S1_VARIANTS(ACT_ID, false, IN_F32, OUT_QUANT),
     S1_VARIANTS(ACT_ID, false, IN_IDX, OUT_F32),
     S1_VARIANTS(ACT_ID, false, IN_F32, OUT_F32),
+    S1_WINO(ACT_RELU, false, IN_F32, OUT_F32),
+    S1_WINO(ACT_RELU, true, IN_F32, OUT_F32),
+    S1_WINO(ACT_ID, false, IN_F32, OUT_QUANT),
+    S1_WINO(ACT_ID, false, IN_IDX, OUT_F32),
+    S1_WINO(ACT_ID, false, IN_F32, OUT_F32),
 };
 const ConvEntry* conv_registry_s1(int* count) {
   *count = sizeof(kS1) / sizeof(kS1[0]);

@@ -134,51 +134,71 @@ int same_pad(int kind, int h) {
 
 // Pick a compiled tiling for this layer: the largest per-workgroup tile that still
 // gives >= 2 workgroups per CU (512 on MI355X); otherwise the variant with the most
-// workgroups.  TIC_FORCE_TILE="th,nsplit" overrides (tuning experiments).
+// workgroups.  `form` 1 selects the Winograd variants of stride-1 layers (weight source 4)
+// where compiled, 0 the direct ones.  TIC_FORCE_TILE="th,nsplit[,wsrc[,wr]]" overrides
+// (tuning experiments, tests); a forced weight source also overrides the form.
+bool form_match(const tic::ConvEntry& c, int form, int fwl) {
+  if (fwl >= 0) return c.wlds == fwl;
+  if (c.wlds == 3) return false;  // persistent variants: only by autotune or forced
+  return (c.wlds == 4) == (form == 1);
+}
+
 const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, int in, int outm, int hg = 0,
-                                int wg = 0, int n = 0) {
+                                int wg = 0, int n = 0, int form = 0) {
   const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
                                            tic::conv_registry_t2};
   int cnt = 0;
   const tic::ConvEntry* e = regs[mode](&cnt);
-  int fth = 0, fns = 0, fwl = -1;
-  if (const char* f = getenv("TIC_FORCE_TILE")) sscanf(f, "%d,%d,%d", &fth, &fns, &fwl);
-  const tic::ConvEntry* best = nullptr;
-  long best_wgs = -1, best_work = -1;
-  bool best_ok = false;
-  for (int i = 0; i < cnt; ++i) {
-    const tic::ConvEntry& c = e[i];
-    if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
-    if (fth && (c.th != fth || c.nsplit != fns || (fwl >= 0 && c.wlds != fwl))) continue;
-    if (c.wlds == 3 && fwl != 3) continue;  // persistent variants: only by autotune or forced
-    const long wgs = (long)((wg + 15) / 16) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
-    const long work = (long)c.th * 64 / c.nsplit;  // pixels x channel-fraction per workgroup
-    const bool ok = wgs >= 512;
-    bool better;
-    if (!best) better = true;
-    else if (ok != best_ok) better = ok;
-    else if (ok) better = work > best_work || (work == best_work && wgs > best_wgs);
-    else better = wgs > best_wgs || (wgs == best_wgs && work > best_work);
-    if (better) {
-      best = &c;
-      best_wgs = wgs;
-      best_work = work;
-      best_ok = ok;
+  int fth = 0, fns = 0, fwl = -1, fwr = 0;
+  if (const char* f = getenv("TIC_FORCE_TILE")) sscanf(f, "%d,%d,%d,%d", &fth, &fns, &fwl, &fwr);
+  if (!fth) fwl = -1;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int fm = pass == 0 ? form : 0;  // no Winograd variant for this signature: direct
+    if (pass == 1 && (form == 0 || fwl >= 0)) break;
+    const tic::ConvEntry* best = nullptr;
+    long best_wgs = -1, best_work = -1;
+    bool best_ok = false;
+    for (int i = 0; i < cnt; ++i) {
+      const tic::ConvEntry& c = e[i];
+      if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
+      if (fth && (c.th != fth || c.nsplit != fns || (fwr > 0 && c.wr != fwr))) continue;
+      if (!form_match(c, fm, fwl)) continue;
+      const int cols = c.wlds == 4 ? 32 * c.wr / (c.th / 2) : 16;  // output columns per workgroup
+      const long wgs = (long)((wg + cols - 1) / cols) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
+      const long work = (long)c.th * cols * 4 / c.nsplit;  // pixels x channel-fraction per workgroup
+      const bool ok = wgs >= 512;
+      bool better;
+      if (!best) better = true;
+      else if (ok != best_ok) better = ok;
+      else if (ok) better = work > best_work || (work == best_work && wgs > best_wgs);
+      else better = wgs > best_wgs || (wgs == best_wgs && work > best_work);
+      if (better) {
+        best = &c;
+        best_wgs = wgs;
+        best_work = work;
+        best_ok = ok;
+      }
     }
+    if (best) return best;
   }
-  return best;
+  return nullptr;
 }
 
-std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, int act, int res, int in, int outm) {
+// Every compiled tiling of this layer signature within one form (all bit-identical).
+std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, int act, int res, int in, int outm,
+                                                   int form = 0) {
   const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
                                            tic::conv_registry_t2};
   int cnt = 0;
   const tic::ConvEntry* e = regs[mode](&cnt);
   std::vector<const tic::ConvEntry*> out;
-  for (int i = 0; i < cnt; ++i)
-    if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
-        e[i].out == outm)
-      out.push_back(&e[i]);
+  for (int pass = 0; pass < 2 && out.empty(); ++pass) {
+    const int fm = pass == 0 ? form : 0;
+    for (int i = 0; i < cnt; ++i)
+      if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
+          e[i].out == outm && (e[i].wlds == 4) == (fm == 1))
+        out.push_back(&e[i]);
+  }
   return out;
 }
 
@@ -197,6 +217,28 @@ void pack_generic(const float* k, int kind, int cin, int cout, std::vector<float
                                          : k[((size_t)tap * cin + ci) * cout + co];  // HWIO
             (*wp)[((((size_t)tap * KC + kc) * 4 + g) * cout + co) * 4 + t] = v;
           }
+}
+
+// Winograd F(2x2,3x3) weights U = G g G^T per (ci, co), in double and rounded once, packed
+// [16 p = 4 xi + nu][Cin/16][4 g][Cout][4 t] (ci = 16 kc + 4 g + t); HWIO input.
+void pack_wino(const float* k, int cin, int cout, std::vector<float>* wp) {
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  const int KC = cin / 16;
+  wp->assign((size_t)16 * cin * cout, 0.f);
+  for (int ci = 0; ci < cin; ++ci)
+    for (int co = 0; co < cout; ++co) {
+      double g[3][3];
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx) g[ky][kx] = k[((size_t)(ky * 3 + kx) * cin + ci) * cout + co];
+      const int kc = ci / 16, gg = (ci % 16) / 4, t = ci % 4;
+      for (int xi = 0; xi < 4; ++xi)
+        for (int nu = 0; nu < 4; ++nu) {
+          double u = 0;
+          for (int ky = 0; ky < 3; ++ky)
+            for (int kx = 0; kx < 3; ++kx) u += G[xi][ky] * g[ky][kx] * G[nu][kx];
+          (*wp)[((((size_t)(xi * 4 + nu) * KC + kc) * 4 + gg) * cout + co) * 4 + t] = (float)u;
+        }
+    }
 }
 
 // First layer: [Cout][4 g][8 t], k = 4t + g -> (tap, c) = divmod(k, 3); k = 27 -> 0.
@@ -258,6 +300,7 @@ struct LayerRT {
   float* d_w = nullptr;
   float* d_w2 = nullptr;  // alternate packing (last layer: scatter form)
   float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
+  float* d_ww = nullptr;  // stride-1 layers: Winograd-packed U (conv3x3_wino.h)
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
@@ -305,6 +348,7 @@ struct tic_handle {
   bool use_graph = false;
   bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); measured slower, opt-in
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
+  int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
   struct GraphKey {
     const void *in, *idx, *rgb;
     int n, nlanes;
@@ -315,6 +359,14 @@ struct tic_handle {
   std::map<GraphKey, hipGraphExec_t> graphs;  // captured encode->decode sequences
   bool rmbe() const { return model_id == TIC_MODEL_RMBE; }
 };
+
+// Key of a layer's tuned-tiling map: the batch size, per stride-1 form (each form has its
+// own candidate set, so switching the form never reuses the other form's choice).
+static int tkey(const tic_handle* h, const LayerRT& l, int n) {
+  return l.def.kind == K_S1 && h->s1_form == 1 ? n + (1 << 24) : n;
+}
+static int layer_form(const tic_handle* h, const LayerRT& l) { return l.def.kind == K_S1 ? h->s1_form : 0; }
+static const float* conv_weights(const LayerRT& l, const tic::ConvEntry* e) { return e->wlds == 4 ? l.d_ww : l.d_w; }
 
 namespace {
 
@@ -383,6 +435,16 @@ int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(i
 }
 
 const int kRgbInDefault = 2;   // TH 16
+
+// Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino, else built-in.
+const int kS1FormDefault = 1;
+int default_s1_form() {
+  const char* f = getenv("TIC_S1_FORM");
+  const std::string s = f ? f : "";
+  if (s == "wino") return 1;
+  if (s == "direct") return 0;
+  return kS1FormDefault;
+}
 
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
 // each form has its own summation order.  Default: the VALU form (variants 6-8);
@@ -545,9 +607,9 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       const int outm = last_enc ? tic::OUT_QUANT : tic::OUT_F32;
       const int hg = d.kind == K_T2 ? lay.h_in : lay.h_out;
       const tic::ConvEntry* e = nullptr;
-      auto it = lay.tuned.find(n);
+      auto it = lay.tuned.find(tkey(h, lay, n));
       if (it != lay.tuned.end()) e = it->second;
-      else e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, hg, hg, n);
+      else e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, hg, hg, n, layer_form(h, lay));
       if (!e)
         return fail(TIC_EUNSUPPORTED, "no kernel for layer %s (kind %d %d->%d act %d res %d in %d out %d)",
                     d.name.c_str(), d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
@@ -567,13 +629,14 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.grid_cap = h->persist_grid;
       if (h->tune_reps > 0 && it == lay.tuned.end()) {
         // time every compiled tiling on the live buffers (re-launching is idempotent)
-        auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm);
+        auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, layer_form(h, lay));
         hipEvent_t t0, t1;
         HIP_TRY(hipEventCreate(&t0));
         HIP_TRY(hipEventCreate(&t1));
         float best_ms = 1e30f;
         const bool log = getenv("TIC_TUNE_LOG") != nullptr;
         for (const tic::ConvEntry* c : cands) {
+          a.wp = conv_weights(lay, c);
           c->fn(a, n, st);  // warm
           HIP_TRY(hipEventRecord(t0, st));
           for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, st);
@@ -593,8 +656,9 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         (void)hipEventDestroy(t1);
         int rc = check_launch();
         if (rc) return rc;
-        lay.tuned[n] = e;
+        lay.tuned[tkey(h, lay, n)] = e;
       }
+      a.wp = conv_weights(lay, e);
       e->fn(a, n, st);
     }
     int rc = check_launch();
@@ -784,6 +848,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   h->act_elems = act;
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(2, std::max(1, atoi(c)));
+  h->s1_form = default_s1_form();
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->lanes[1].stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
@@ -805,6 +870,7 @@ void tic_destroy(tic_handle* h) {
     if (l.d_w) (void)hipFree(l.d_w);
     if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_w3) (void)hipFree(l.d_w3);
+    if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
@@ -892,8 +958,15 @@ int tic_finalize(tic_handle* h) {
     if (l.d_w) (void)hipFree(l.d_w);
     if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_w3) (void)hipFree(l.d_w3);
+    if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_b) (void)hipFree(l.d_b);
-    l.d_w = l.d_w2 = l.d_w3 = l.d_b = nullptr;
+    l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_b = nullptr;
+    if (l.def.kind == K_S1 && i > 0 && i < L - 1) {
+      std::vector<float> ww;
+      pack_wino(l.k.data(), l.def.cin, l.def.cout, &ww);
+      HIP_TRY(hipMalloc((void**)&l.d_ww, ww.size() * sizeof(float)));
+      HIP_TRY(hipMemcpy(l.d_ww, ww.data(), ww.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     if (i == L - 1) {
       std::vector<float> w2;
       pack_rgb_out_scatter(l.k.data(), l.def.cin, &w2);
@@ -1049,6 +1122,13 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->use_graph = value != 0;
     return TIC_OK;
   }
+  if (k == "s1_form") {  // 0 direct, 1 Winograd, -1 the default (TIC_S1_FORM or built-in)
+    if (value < -1 || value > 1) return fail(TIC_EINVAL, "s1_form must be -1, 0 or 1");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->s1_form = value < 0 ? default_s1_form() : value;
+    return TIC_OK;
+  }
   return fail(TIC_EINVAL, "unknown option %s", key);
 }
 
@@ -1175,7 +1255,7 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
   if (!d_in || n <= 0 || reps <= 0) return fail(TIC_EINVAL, "bad arguments");
   if (n > h->chunk) return fail(TIC_EINVAL, "autotune n %d exceeds chunk %d", n, h->chunk);
   for (auto& l : h->layers) {
-    l.tuned.erase(n);
+    l.tuned.erase(tkey(h, l, n));
     l.tuned_var.erase(n);
     l.tuned_var.erase(-n);
   }
@@ -1225,7 +1305,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     for (size_t i = 0; i < h->layers.size(); ++i) {
       const LayerRT& l = h->layers[i];
       const bool rgb = i == 0 || i + 1 == h->layers.size();
-      if (rgb ? !l.tuned_var.count(m) : !l.tuned.count(m)) have = false;
+      if (rgb ? !l.tuned_var.count(m) : !l.tuned.count(tkey(h, l, m))) have = false;
     }
     if (!have) {
       rc = tic_autotune(h, d_in, m, reps);
@@ -1295,13 +1375,13 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       } else {
         const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
-                                     last_enc ? tic::OUT_QUANT : tic::OUT_F32);
-        const tic::ConvEntry* keep = l.tuned[sizes[0]];
+                                     last_enc ? tic::OUT_QUANT : tic::OUT_F32, layer_form(h, l));
+        const tic::ConvEntry* keep = l.tuned[tkey(h, l, sizes[0])];
         const tic::ConvEntry* best_e = keep;
         float best = cur;
         for (const tic::ConvEntry* c : cands) {
           if (c == keep || rc) continue;
-          for (int m : sizes) l.tuned[m] = c;
+          for (int m : sizes) l.tuned[tkey(h, l, m)] = c;
           float ms = 0.f;
           rc = measure(&ms);
           if (log)
@@ -1312,7 +1392,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
             best_e = c;
           }
         }
-        for (int m : sizes) l.tuned[m] = best_e;
+        for (int m : sizes) l.tuned[tkey(h, l, m)] = best_e;
         cur = best;
       }
     }
@@ -1343,7 +1423,7 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
     *nsplit = i == L - 1 ? v / 3 : 0;  // last layer: 0 dense, 1 scatter, 2 VALU, 3 VALU persistent
     return TIC_OK;
   }
-  auto it = l.tuned.find(n);
+  auto it = l.tuned.find(tkey(h, l, n));
   const tic::ConvEntry* e = nullptr;
   if (it != l.tuned.end()) {
     e = it->second;
@@ -1352,7 +1432,7 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
     const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
     const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
     e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
-                  last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n);
+                  last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
   }
   if (e) {
     *th = e->th;
@@ -1391,13 +1471,16 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   } else {
     const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
     const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
-    auto it = l.tuned.find(n);
+    auto it = l.tuned.find(tkey(h, l, n));
     const tic::ConvEntry* e =
         it != l.tuned.end() ? it->second
                             : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
-                                        last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n);
+                                        last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
-    if (e->wlds == 3)
+    if (e->wlds == 4)
+      snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
+               e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
+    else if (e->wlds == 3)
       snprintf(buf, sizeof buf, "conv3x3_persist_kernel<%d,%d,%d,%d,%d,%d>", e->mode, e->cin, e->cout, e->th, e->wr,
                e->act);
     else
@@ -1418,12 +1501,14 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
     return fail(TIC_EINVAL, "bad arguments");
   HIP_TRY(hipSetDevice(h->device));
   const tic::ConvEntry* e = find_conv(kind, cin, cout, act, d_res ? 1 : 0, tic::IN_F32, tic::OUT_F32,
-                                      kind == K_T2 ? H : out_size(kind, H), kind == K_T2 ? W : out_size(kind, W), n);
+                                      kind == K_T2 ? H : out_size(kind, H), kind == K_T2 ? W : out_size(kind, W), n,
+                                      kind == K_S1 ? h->s1_form : 0);
   if (!e)
     return fail(TIC_EUNSUPPORTED, "no compiled conv3x3 for kind %d %d->%d act %d res %d", kind, cin, cout, act,
                 d_res ? 1 : 0);
   std::vector<float> wp;
-  pack_generic(w_host, kind, cin, cout, &wp);
+  if (e->wlds == 4) pack_wino(w_host, cin, cout, &wp);
+  else pack_generic(w_host, kind, cin, cout, &wp);
   float *d_w = nullptr, *d_b = nullptr;
   HIP_TRY(hipMalloc((void**)&d_w, wp.size() * 4));
   HIP_TRY(hipMalloc((void**)&d_b, (size_t)cout * 4));
