@@ -17,8 +17,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 
 
+PREFIX = os.environ.get("PMC_PREFIX", "pmc")
+
+
 def load(kind):
-    path = os.path.join(OUT, f"pmc_{kind}", "p_counter_collection.csv")
+    path = os.path.join(OUT, f"{PREFIX}_{kind}", "p_counter_collection.csv")
     per = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
     if not os.path.exists(path):
