@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="execution lanes per GPU (1 or 2)")
+    ap.add_argument("--streams", type=int, default=2, help="execution lanes (HIP streams) per GPU, 1..4")
     ap.add_argument("--tune-step", type=int, default=1,
                     help="rounds of in-situ (whole dual-lane step) tuning after the per-layer autotune; 0 = off")
     ap.add_argument("--graph", action="store_true", help="replay the launch sequence as a HIP graph (opt-in)")
@@ -195,7 +195,7 @@ def main():
     d_rgb = codec.alloc(x.nbytes)
 
     # per-lane batch: with 2 lanes each kernel launch processes half the batch
-    lane_b = (B + 1) // 2 if args.streams == 2 and B > 1 else B
+    lane_b = -(-B // max(1, min(args.streams, B)))  # largest per-lane part of the batch
     if not args.no_autotune:
         codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice, outside the timed region
         if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
@@ -365,9 +365,9 @@ def main_image(args):
     d_sym = [codec.alloc(npat * eh * ew * ec) for _ in range(NI)]
     d_out = [codec.alloc(H * W * 3) for _ in range(NI)]
 
-    lane_b = (npat + 1) // 2 if args.streams == 2 else npat
+    lane_b = -(-npat // max(1, min(args.streams, npat)))
     n_win = (H // 128) * ((W - 64) // 128) + ((H - 64) // 128) * (W // 128)
-    win_lane = (min(n_win, 256) + 1) // 2 if args.streams == 2 else min(n_win, 256)
+    win_lane = -(-min(n_win, 256) // max(1, min(args.streams, min(n_win, 256))))
     d_pat = codec.alloc(npat * P * P * 3)
     codec.image_to_patches_device(d_img[0], H, W, P, d_pat)
     d_win = post.alloc(win_lane * 128 * 128 * 3 * 4)

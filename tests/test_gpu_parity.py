@@ -359,3 +359,19 @@ def test_codec_vs_golden_fixture(name):
     assert int(np.count_nonzero((idx != z["idx"]) & safe)) == 0
     du = np.abs(rgb.astype(np.int16) - z["recon_u8"].astype(np.int16))
     assert int(du.max()) <= 1 and float(np.mean(du > 0)) < 1e-3
+
+
+def test_lanes_bit_identical(lib_codec):
+    """Splitting a chunk over 1..4 lanes (HIP streams) changes nothing in the results."""
+    codec, _ = lib_codec(0, 64)
+    x = structured_patches(7, 64, seed=71)
+    outs = []
+    try:
+        for k in (1, 2, 3, 4):
+            codec.set_option("streams", k)
+            idx = codec.encode(x)
+            outs.append((idx, codec.decode(idx)))
+    finally:
+        codec.set_option("streams", 2)
+    for idx, rgb in outs[1:]:
+        assert np.array_equal(idx, outs[0][0]) and np.array_equal(rgb, outs[0][1])

@@ -319,9 +319,9 @@ struct Lane {
 struct tic_handle {
   int model_id = 0, P = 0, Q = 2, device = 0;
   hipStream_t stream = nullptr;
-  Lane lanes[2];
-  int nlanes = 2;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  Lane lanes[4];
+  int nlanes = 2;  // lanes a chunk is split over (1..4)
+  hipEvent_t ev_fork = nullptr, ev_join[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<LayerRT> layers;
   int n_enc = 0;
   float mean[3] = {0, 0, 0}, std[3] = {1, 1, 1};
@@ -683,24 +683,33 @@ size_t code_elems(const tic_handle* h) {
 }
 
 // chunked drivers (device pointers).  Each chunk runs on lane 0, or is split in halves
-// over both lanes (fork/join with events on the handle's stream) when nlanes == 2.
+// over nlanes lanes in near-equal parts (fork/join with events on the handle's stream).
 template <typename F>
 int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
-  if (h->nlanes < 2 || !allow_split || m < 2) {
+  const int k = allow_split ? std::min(h->nlanes, m) : 1;
+  if (k < 2) {
     int rc = ensure_ws(h, h->lanes[0], m);
     if (rc) return rc;
     return body(h->lanes[0], 0, m);
   }
-  const int m0 = (m + 1) / 2, m1 = m - m0;
-  int rc = ensure_ws(h, h->lanes[0], m0);
-  if (!rc) rc = ensure_ws(h, h->lanes[1], m1);
-  if (rc) return rc;
+  int part[4], off[4];
+  for (int i = 0, o = 0; i < k; ++i) {
+    part[i] = m / k + (i < m % k ? 1 : 0);
+    off[i] = o;
+    o += part[i];
+  }
+  for (int i = 0; i < k; ++i) {
+    int rc = ensure_ws(h, h->lanes[i], part[i]);
+    if (rc) return rc;
+  }
   HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-  HIP_TRY(hipStreamWaitEvent(h->lanes[1].stream, h->ev_fork, 0));
-  rc = body(h->lanes[0], 0, m0);
-  if (!rc) rc = body(h->lanes[1], m0, m1);
-  HIP_TRY(hipEventRecord(h->ev_join, h->lanes[1].stream));
-  HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  for (int i = 1; i < k; ++i) HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
+  int rc = TIC_OK;
+  for (int i = 0; i < k && !rc; ++i) rc = body(h->lanes[i], off[i], part[i]);
+  for (int i = 1; i < k; ++i) {
+    HIP_TRY(hipEventRecord(h->ev_join[i], h->lanes[i].stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join[i], 0));
+  }
   return rc;
 }
 
@@ -847,12 +856,14 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   }
   h->act_elems = act;
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
-  if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(2, std::max(1, atoi(c)));
+  if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
   h->s1_form = default_s1_form();
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->lanes[1].stream, hipStreamNonBlocking);
+  for (int i = 1; i < 4 && e == hipSuccess; ++i) {
+    e = hipStreamCreateWithFlags(&h->lanes[i].stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete h;
     return fail(TIC_EHIP, "stream/event creation: %s", hipGetErrorString(e));
@@ -877,12 +888,14 @@ void tic_destroy(tic_handle* h) {
   for (auto& ln : h->lanes)
     for (auto& b : ln.ws)
       if (b) (void)hipFree(b);
-  if (h->lanes[1].stream) {
-    (void)hipStreamSynchronize(h->lanes[1].stream);
-    (void)hipStreamDestroy(h->lanes[1].stream);
+  for (int i = 1; i < 4; ++i) {
+    if (h->lanes[i].stream) {
+      (void)hipStreamSynchronize(h->lanes[i].stream);
+      (void)hipStreamDestroy(h->lanes[i].stream);
+    }
+    if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
   }
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->d_lut) (void)hipFree(h->d_lut);
   if (h->st_in) (void)hipFree(h->st_in);
   if (h->st_out) (void)hipFree(h->st_out);
@@ -1096,7 +1109,7 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
   if (!h || !key) return fail(TIC_EINVAL, "null argument");
   const std::string k(key);
   if (k == "streams") {
-    if (value < 1 || value > 2) return fail(TIC_EINVAL, "streams must be 1 or 2");
+    if (value < 1 || value > 4) return fail(TIC_EINVAL, "streams must be 1..4");
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->nlanes = value;
@@ -1293,11 +1306,10 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   if (n > h->chunk) return fail(TIC_EINVAL, "autotune_step n %d exceeds chunk %d", n, h->chunk);
   // per-launch batch sizes the lanes will see for n
   std::vector<int> sizes;
-  if (h->nlanes >= 2 && n >= 2) {
-    sizes.push_back((n + 1) / 2);
-    if (n / 2 != (n + 1) / 2) sizes.push_back(n / 2);
-  } else {
-    sizes.push_back(n);
+  {
+    const int k = std::max(1, std::min(h->nlanes, n));
+    sizes.push_back((n + k - 1) / k);
+    if (n % k) sizes.push_back(n / k);
   }
   // make sure every layer has a solo-tuned starting point for those sizes
   for (int m : sizes) {

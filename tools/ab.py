@@ -47,7 +47,9 @@ def main():
 
     for cfg in args.cfg:  # autotune each configuration's lane batch once
         apply(cfg)
-        lane_b = (B + 1) // 2 if "streams=1" not in cfg else B
+        m = [int(kv.split("=")[1]) for kv in cfg.split(",") if kv.startswith("streams=")]
+        k = m[-1] if m else 2
+        lane_b = -(-B // max(1, min(k, B)))
         codec.autotune(d_in, lane_b, reps=5)
     res = {c: [] for c in args.cfg}
     for r in range(args.rounds):
