@@ -375,3 +375,38 @@ def test_lanes_bit_identical(lib_codec):
         codec.set_option("streams", 2)
     for idx, rgb in outs[1:]:
         assert np.array_equal(idx, outs[0][0]) and np.array_equal(rgb, outs[0][1])
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 256), (0, 48), (1, 64), (3, 64), (2, 32)])
+def test_fused_tail_bit_identical(lib_codec, monkeypatch, model_id, P):
+    """dec10_kernel (decode_1 + decode_0 through LDS, halo recomputed on the VALU) == the two
+    separate kernels (decode_1 by conv3x3_kernel, decode_0 in the VALU form), bit for bit,
+    bytes and floats, partial edge tiles included (P = 48)."""
+    codec, _ = lib_codec(model_id, P)
+    idx = codec.encode(structured_patches(3, P, seed=81 + model_id))
+    try:
+        codec.set_option("fuse_tail", 0)
+        u0, f0 = codec.decode(idx, return_float=True)
+        codec.set_option("fuse_tail", 1)
+        outs = []
+        for v in ("0", "1"):
+            monkeypatch.setenv("TIC_DEC10_VARIANT", v)
+            outs.append(codec.decode(idx, return_float=True))
+    finally:
+        codec.set_option("fuse_tail", 0)
+    for u1, f1 in outs:
+        assert np.array_equal(u0, u1) and np.array_equal(f0, f1)
+
+
+def test_fused_tail_rmbe_bit_identical():
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import RMBE_ID
+    r = np.random.default_rng(5)
+    win = np.clip(r.normal(120, 50, (3, 128, 128, 3)), 0, 255).astype(np.float32)
+    with Codec(RMBE_ID, synthetic_params(RMBE_ID), SYNTH_MEAN, SYNTH_STD, patch_size=128) as c:
+        c.set_option("fuse_tail", 0)
+        a = c.rmbe_windows(win)
+        c.set_option("fuse_tail", 1)
+        b = c.rmbe_windows(win)
+    assert np.array_equal(a, b)

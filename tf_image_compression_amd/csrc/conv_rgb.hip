@@ -5,6 +5,7 @@
 
 #include "conv3x3.h"
 #include "convT_rgb_valu.h"
+#include "dec10.h"
 
 namespace tic {
 
@@ -117,6 +118,24 @@ static bool rgb_out_c(const RgbOutArgs& a, int n, hipStream_t s, int variant) {
 bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant) {
   if (cin == 32) return rgb_out_c<32>(a, n, s, variant);
   if (cin == 16) return rgb_out_c<16>(a, n, s, variant);
+  return false;
+}
+
+template <int C1, int C0>
+static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
+  dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n);
+  if (variant == 0) hipLaunchKernelGGL((dec10_kernel<C1, C0, false>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((dec10_kernel<C1, C0, true>), grid, dim3(256), 0, s, a);
+  return true;
+}
+
+int dec10_variants() { return 2; }  // decode_0 weights: 0 scalar loads, 1 LDS
+
+bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {
+  if (variant < 0 || variant >= dec10_variants()) return false;
+  if (c1 == 32 && c0 == 32) return dec10_c<32, 32>(a, n, s, variant);
+  if (c1 == 32 && c0 == 16) return dec10_c<32, 16>(a, n, s, variant);
+  if (c1 == 64 && c0 == 32) return dec10_c<64, 32>(a, n, s, variant);
   return false;
 }
 

@@ -68,6 +68,16 @@ struct RgbOutArgs {
   int grid_cap;        // > 0: cap on the persistent grid (tests force several tiles per workgroup)
 };
 
+// decode_1 -> decode_0 fused through LDS (dec10.h).
+struct Dec10Args {
+  const float* in;     // decode_1 input [N,H,W,C1]
+  const float* wp1;    // decode_1 generic packing [tap][C1/16][4 g][C0][4 t]
+  const float* w1raw;  // decode_1 TF kernel as-is, [3][3][C0][C1]
+  const float* b1;     // [C0]
+  int H, W;            // decode_1 input size (decode_0's input is 2H x 2W)
+  RgbOutArgs rgb;      // decode_0: wraw, bias, normalisation, outputs; rgb.H/W = 2H/2W
+};
+
 typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);
 
 struct ConvEntry {
@@ -96,6 +106,10 @@ bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipS
 int rgb_out_variants();
 bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant);
 bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant);
+// decode_1 (C1 -> C0) + decode_0 fused; false if (C1, C0) is not compiled.  Variants are
+// bit-identical (decode_0's weights via scalar loads or LDS).
+int dec10_variants();
+bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant);
 
 // Whole-image glue and the symbol histogram (image_ops.hip).
 void launch_tile_reflect(const uint8_t* img, int H, int W, int P, int hn, int wn, uint8_t* out, int num_cus,

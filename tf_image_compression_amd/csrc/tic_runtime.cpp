@@ -349,6 +349,7 @@ struct tic_handle {
   bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); measured slower, opt-in
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
+  bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   struct GraphKey {
     const void *in, *idx, *rgb;
     int n, nlanes;
@@ -436,6 +437,9 @@ int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(i
 
 const int kRgbInDefault = 2;   // TH 16
 
+// decoder tail fusion default (option "fuse_tail", env TIC_FUSE_TAIL)
+const bool kFuseTailDefault = false;
+
 // Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino, else built-in.
 const int kS1FormDefault = 1;
 int default_s1_form() {
@@ -479,6 +483,16 @@ struct Prof {
 static bool fuses01(const tic_handle* h) {
   return h->fuse01 && h->layers.size() > 2 && h->layers[1].def.kind == K_S2 && h->layers[1].def.act == 1 &&
          !h->layers[1].def.residual && !(!h->rmbe() && h->n_enc == 2);
+}
+
+// decoder's last two layers through one dec10_kernel launch (option "fuse_tail"; only with
+// the VALU last-layer form, whose summation order the fused kernel reproduces)
+static bool fuses_tail(const tic_handle* h) {
+  const int L = (int)h->layers.size();
+  if (!h->fuse_tail || L < 3 || rgb_out_form().lo != 6) return false;
+  const LayerDef& d = h->layers[L - 2].def;
+  const bool ok = (d.cin == 32 && d.cout == 32) || (d.cin == 32 && d.cout == 16) || (d.cin == 64 && d.cout == 32);
+  return ok && d.kind == K_T2 && d.act == 1 && !d.residual && !(!h->rmbe() && L - 2 == h->n_enc);
 }
 
 // Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
@@ -548,6 +562,43 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       cur = dst;
       ++li;  // layer 1 consumed
       continue;
+    }
+    if (li == L - 2 && li + 1 < l1 && fuses_tail(h)) {
+      LayerRT& last_l = h->layers[L - 1];
+      tic::Dec10Args a{};
+      a.in = src;
+      a.wp1 = lay.d_w;
+      a.w1raw = lay.d_w3;
+      a.b1 = lay.d_b;
+      a.H = a.W = lay.h_in;
+      a.rgb.wraw = last_l.d_w3;
+      a.rgb.bias = last_l.d_b;
+      a.rgb.out_u8 = d_rgb;
+      a.rgb.out_f32 = d_f32;
+      a.rgb.H = a.rgb.W = last_l.h_in;
+      for (int c = 0; c < 3; ++c) {
+        a.rgb.mean[c] = h->mean[c];
+        a.rgb.std[c] = h->std[c];
+      }
+      auto it = lay.tuned_var.find(n);  // fused-tail variants keyed by n on layer L-2
+      int var = it != lay.tuned_var.end() ? it->second : 0;
+      if (const char* t = getenv("TIC_DEC10_VARIANT")) var = atoi(t);
+      else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
+        int rc = time_variants(st, tic::dec10_variants(), h->tune_reps,
+                               [&](int v) { return tic::launch_dec10(d.cin, d.cout, a, n, st, v); }, &var, "dec10", n);
+        if (rc) return rc;
+        lay.tuned_var[n] = var;
+      }
+      if (!tic::launch_dec10(d.cin, d.cout, a, n, st, var))
+        return fail(TIC_EUNSUPPORTED, "fused decoder tail %d->%d->3 not compiled", d.cin, d.cout);
+      int rc = check_launch();
+      if (rc) return rc;
+      if (prof.ev) {
+        HIP_TRY(hipEventRecord(prof.ev[2 * li + 1], st));
+        HIP_TRY(hipEventRecord(prof.ev[2 * li + 2], st));  // the last layer ran inside this launch
+        HIP_TRY(hipEventRecord(prof.ev[2 * li + 3], st));
+      }
+      break;
     }
     if (first) {
       tic::RgbInArgs a{};
@@ -858,6 +909,8 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
   h->s1_form = default_s1_form();
+  if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
+  else h->fuse_tail = kFuseTailDefault;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   for (int i = 1; i < 4 && e == hipSuccess; ++i) {
     e = hipStreamCreateWithFlags(&h->lanes[i].stream, hipStreamNonBlocking);
@@ -979,6 +1032,10 @@ int tic_finalize(tic_handle* h) {
       pack_wino(l.k.data(), l.def.cin, l.def.cout, &ww);
       HIP_TRY(hipMalloc((void**)&l.d_ww, ww.size() * sizeof(float)));
       HIP_TRY(hipMemcpy(l.d_ww, ww.data(), ww.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    if (i == L - 2 && l.def.kind == K_T2) {  // raw kernel for the fused decoder tail's halo
+      HIP_TRY(hipMalloc((void**)&l.d_w3, l.k.size() * sizeof(float)));
+      HIP_TRY(hipMemcpy(l.d_w3, l.k.data(), l.k.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     if (i == L - 1) {
       std::vector<float> w2;
@@ -1133,6 +1190,12 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
   }
   if (k == "graph") {
     h->use_graph = value != 0;
+    return TIC_OK;
+  }
+  if (k == "fuse_tail") {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->fuse_tail = value != 0;
     return TIC_OK;
   }
   if (k == "s1_form") {  // 0 direct, 1 Winograd, -1 the default (TIC_S1_FORM or built-in)
@@ -1317,6 +1380,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     for (size_t i = 0; i < h->layers.size(); ++i) {
       const LayerRT& l = h->layers[i];
       const bool rgb = i == 0 || i + 1 == h->layers.size();
+      if (i + 2 >= h->layers.size() && fuses_tail(h)) continue;  // runs inside dec10_kernel
       if (rgb ? !l.tuned_var.count(m) : !l.tuned.count(tkey(h, l, m))) have = false;
     }
     if (!have) {
@@ -1359,6 +1423,23 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   float cur = 0.f;
   rc = measure(&cur);
   if (log && !rc) fprintf(stderr, "tune-step n=%d start: %.2f us\n", n, 1e3f * cur);
+  // structural, bit-identical choice first: the decoder tail fused (dec10_kernel) or not
+  if (!rc && !getenv("TIC_FUSE_TAIL")) {
+    const bool was = h->fuse_tail;
+    h->fuse_tail = true;
+    const bool can = fuses_tail(h);
+    h->fuse_tail = was;
+    if (can) {
+      h->fuse_tail = !was;
+      clear_graphs(h);
+      float alt = 0.f;
+      rc = measure(&alt);
+      if (log && !rc) fprintf(stderr, "tune-step fuse_tail=%d : %.2f us\n", (int)h->fuse_tail, 1e3f * alt);
+      if (!rc && alt < cur) cur = alt;
+      else h->fuse_tail = was;
+      clear_graphs(h);
+    }
+  }
   const int L = (int)h->layers.size();
   for (int round = 0; round < rounds && !rc; ++round) {
     for (int i = 0; i < L && !rc; ++i) {
@@ -1366,6 +1447,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       const LayerDef& d = l.def;
       const bool first = i == 0, last = i == L - 1;
       if ((first || i == 1) && fuses01(h)) continue;
+      if (i >= L - 2 && fuses_tail(h)) continue;
       if (first || last) {
         const RgbOutForm fm = first ? RgbOutForm{0, tic::rgb_in_variants()} : rgb_out_form();
         const int keep = first ? l.tuned_var[sizes[0]] : rgb_out_variant(l.tuned_var, sizes[0]);
@@ -1461,7 +1543,9 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   const int L = (int)h->layers.size();
   const char* tf[2] = {"false", "true"};
   char buf[160] = "";
-  if (fuses01(h) && (i == 0 || i == 1)) {
+  if (fuses_tail(h) && i >= L - 2) {
+    if (i == L - 2) snprintf(buf, sizeof buf, "dec10_kernel<%d,%d>", d.cin, d.cout);
+  } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
       auto iv = l.tuned_var.find(-n);
       const int v = iv != l.tuned_var.end() ? iv->second : 1;
