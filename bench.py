@@ -59,8 +59,11 @@ def parse():
     return args
 
 
-def kernel_groups(codec, model_id, P, ms):
-    """Group layers by the kernel instance they launch (same template args + shape)."""
+def kernel_groups(codec, model_id, P, ms, kernels=None):
+    """Group layers by the kernel instance they launch (same template args + shape).  A
+    layer whose kernel name is '' ran inside the previous layer's launch (enc01_kernel,
+    dec10_kernel): the pair is one group, its work the sum of both minus the intermediate
+    activation that never reaches HBM (written and read once in the unfused form)."""
     from tf_image_compression_amd.topology import layer_work, RMBE_ID, weight_bytes
     work = layer_work(model_id, P)
     L = len(work)
@@ -75,17 +78,33 @@ def kernel_groups(codec, model_id, P, ms):
         rows.append({"layer": lay.name, "kind": lay.kind, "cin": lay.cin, "cout": lay.cout, "out_hw": ho,
                      "ms": float(ms[i]), "flops_per_patch": flops, "bytes_per_patch": nbytes,
                      "weight_bytes": weight_bytes(lay), "key": list(map(str, key))})
-        g = groups.setdefault(key, {"layers": [], "ms": 0.0, "flops": flops, "bytes": nbytes,
-                                    "wbytes": weight_bytes(lay)})
-        g["layers"].append(lay.name)
-        g["ms"] += float(ms[i])
+    i = 0
+    while i < L:
+        lay, flops, nbytes, ho = work[i]
+        r = rows[i]
+        key, names = tuple(r["key"]), [lay.name]
+        f, b, wb, t = flops, nbytes, weight_bytes(lay), float(ms[i])
+        if kernels is not None and i + 1 < L and kernels[i + 1] == "":
+            nl, nf, nb_, nho = work[i + 1]
+            f += nf
+            b += nb_ - 2 * ho * ho * lay.cout * 4  # the f32 intermediate stays on chip
+            wb += weight_bytes(nl)
+            t += float(ms[i + 1])
+            names.append(nl.name)
+            key = key + ("fused", nl.name)
+            i += 1
+        g = groups.setdefault(key, {"layers": [], "ms": 0.0, "flops": f, "bytes": b, "wbytes": wb, "launches": 0})
+        g["layers"].extend(names)
+        g["ms"] += t
+        g["launches"] += 1
+        i += 1
     return groups, rows
 
 
 def roofline_of(group, batch):
     flops = group["flops"] * batch
     nbytes = group["bytes"] * batch + group["wbytes"]
-    ms = group["ms"] / len(group["layers"])  # mean duration per launch
+    ms = group["ms"] / group.get("launches", len(group["layers"]))  # mean duration per launch
     t_c = flops / (PEAK_FP32_TFLOPS * 1e12)
     t_m = nbytes / (PEAK_HBM_GBS * 1e9)
     if t_m > t_c:
@@ -227,14 +246,14 @@ def main():
     # per-layer kernel timing: HIP events around each launch on the lane's stream, at the
     # per-launch batch (lane_b), outside the timed region
     ms = codec.profile_layers(d_in, lane_b, args.profile_iters)
-    groups, rows = kernel_groups(codec, M, P, ms)
+    kernels = codec.layer_kernels(lane_b)
+    groups, rows = kernel_groups(codec, M, P, ms, kernels)
     dom_key = max(groups, key=lambda k: groups[k]["ms"])
     roof, dom_ms, dom_flops, dom_bytes = roofline_of(groups[dom_key], lane_b)
     # HBM bytes per launch of the dominant kernel instance from the committed PMC summary
     # (tools/pmc_box.sh + tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
-    kernels = codec.layer_kernels(lane_b)
     names = {lay.name: i for i, lay in enumerate(layer_table(M))}
-    dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]})
+    dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
     roof["traffic"] = None
     roof["traffic_source"] = None
     if os.path.exists(args.traffic):
@@ -407,8 +426,8 @@ def main_image(args):
     # per-layer HIP-event timing of both networks at their per-launch batch sizes
     ms_c = codec.profile_layers(d_pat, lane_b, args.profile_iters)
     ms_r = post.profile_layers(d_win, win_lane, args.profile_iters)
-    groups, rows = kernel_groups(codec, M, P, ms_c)
-    rgroups, rrows = kernel_groups(post, RMBE_ID, 128, ms_r)
+    groups, rows = kernel_groups(codec, M, P, ms_c, codec.layer_kernels(lane_b))
+    rgroups, rrows = kernel_groups(post, RMBE_ID, 128, ms_r, post.layer_kernels(win_lane))
     # dominant = largest time per image: per-launch ms x launches per image
     per_img = {("codec",) + k: (g, lane_b, npat) for k, g in groups.items()}
     per_img.update({("rmbe",) + k: (g, win_lane, n_win) for k, g in rgroups.items()})
@@ -421,7 +440,7 @@ def main_image(args):
     net, net_id = (post, RMBE_ID) if dom_key[0] == "rmbe" else (codec, M)
     kern = net.layer_kernels(lb)
     idx = {lay.name: i for i, lay in enumerate(layer_table(net_id))}
-    dom_kernels = sorted({kern[idx[nm]] for nm in g["layers"]})
+    dom_kernels = sorted({kern[idx[nm]] for nm in g["layers"]} - {""})
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
     roof["kernel_instance"] = dom_kernels
     roof["kernel"] = ("rmbe:" if dom_key[0] == "rmbe" else f"model_{M}:") + "+".join(g["layers"])
