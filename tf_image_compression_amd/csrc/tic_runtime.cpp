@@ -1423,22 +1423,31 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   float cur = 0.f;
   rc = measure(&cur);
   if (log && !rc) fprintf(stderr, "tune-step n=%d start: %.2f us\n", n, 1e3f * cur);
-  // structural, bit-identical choice first: the decoder tail fused (dec10_kernel) or not
-  if (!rc && !getenv("TIC_FUSE_TAIL")) {
-    const bool was = h->fuse_tail;
-    h->fuse_tail = true;
-    const bool can = fuses_tail(h);
-    h->fuse_tail = was;
-    if (can) {
-      h->fuse_tail = !was;
-      clear_graphs(h);
-      float alt = 0.f;
-      rc = measure(&alt);
-      if (log && !rc) fprintf(stderr, "tune-step fuse_tail=%d : %.2f us\n", (int)h->fuse_tail, 1e3f * alt);
-      if (!rc && alt < cur) cur = alt;
-      else h->fuse_tail = was;
-      clear_graphs(h);
-    }
+  // structural, bit-identical choices first: the decoder tail fused (dec10_kernel) or not,
+  // the first two layers fused (enc01_kernel) or not — kept only where the step is faster
+  struct Flag {
+    bool* v;
+    bool (*applies)(const tic_handle*);
+    const char* env;
+    const char* name;
+  };
+  const Flag flags[2] = {{&h->fuse_tail, fuses_tail, "TIC_FUSE_TAIL", "fuse_tail"},
+                         {&h->fuse01, fuses01, "TIC_FUSE01", "fuse01"}};
+  for (const Flag& f : flags) {
+    if (rc || getenv(f.env)) continue;
+    const bool was = *f.v;
+    *f.v = true;
+    const bool can = f.applies(h);
+    *f.v = was;
+    if (!can) continue;
+    *f.v = !was;
+    clear_graphs(h);
+    float alt = 0.f;
+    rc = measure(&alt);
+    if (log && !rc) fprintf(stderr, "tune-step %s=%d : %.2f us\n", f.name, (int)*f.v, 1e3f * alt);
+    if (!rc && alt < cur) cur = alt;
+    else *f.v = was;
+    clear_graphs(h);
   }
   const int L = (int)h->layers.size();
   for (int round = 0; round < rounds && !rc; ++round) {
