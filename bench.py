@@ -442,6 +442,17 @@ def main_image(args):
     idx = {lay.name: i for i, lay in enumerate(layer_table(net_id))}
     dom_kernels = sorted({kern[idx[nm]] for nm in g["layers"]} - {""})
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
+    # HBM bytes per launch from the PMC summaries (tools/pmc_round.sh); the PMC runs launch
+    # 32 (configs[1]) or 128 (configs[2]) patches per kernel, this workload lb: scaled
+    for path in (args.traffic, os.path.join(ROOT, "profiles", "traffic_r01_model3.json")):
+        if roof["traffic"] is None and os.path.exists(path):
+            tr = json.load(open(path))
+            ents = [tr[k] for k in dom_kernels if k in tr]
+            if ents:
+                pmc_lane = 128 if "model3" in path else 32  # patches per launch in the PMC run
+                roof["traffic"] = round(float(np.mean([e["bytes"] for e in ents])) * lb / pmc_lane)
+                roof["traffic_source"] = os.path.relpath(path, ROOT)
+                roof["traffic_note"] = f"PMC bytes per launch at {pmc_lane} patches, scaled to {lb}"
     roof["kernel_instance"] = dom_kernels
     roof["kernel"] = ("rmbe:" if dom_key[0] == "rmbe" else f"model_{M}:") + "+".join(g["layers"])
     roof["ms_per_launch"] = round(dom_ms, 5)

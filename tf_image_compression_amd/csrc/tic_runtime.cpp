@@ -1553,7 +1553,12 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   const char* tf[2] = {"false", "true"};
   char buf[160] = "";
   if (fuses_tail(h) && i >= L - 2) {
-    if (i == L - 2) snprintf(buf, sizeof buf, "dec10_kernel<%d,%d>", d.cin, d.cout);
+    if (i == L - 2) {
+      auto iv = l.tuned_var.find(n);
+      int v = iv != l.tuned_var.end() ? iv->second : 0;
+      if (const char* t = getenv("TIC_DEC10_VARIANT")) v = atoi(t);
+      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s>", d.cin, d.cout, tf[v == 1]);
+    }
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
       auto iv = l.tuned_var.find(-n);
