@@ -35,6 +35,7 @@ namespace tic {
 template <int CIN, int PS, int LC>
 __device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, float (&acc)[4][3]) {
   constexpr int C4 = CIN / 4;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int off = 0; off < 4; ++off) {
     const int dy = -(off >> 1), dx = -(off & 1);
@@ -48,23 +49,40 @@ __device__ __forceinline__ void rgb_out_fma(const float* self, const float* __re
       x[4 * c4 + 2] = v.z;
       x[4 * c4 + 3] = v.w;
     }
+    // phases using this offset, paired so one packed fma (v_pk_fma_f32) advances two
+    // outputs' chains by one step each — every output's own fma order is unchanged
+    int ph[4], np = 0;
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      const int py = ph >> 1, px = ph & 1;
-      if ((dy != 0 && py == 1) || (dx != 0 && px == 1)) continue;  // phase does not use this offset
-      const int ky = py ? 1 : (dy == 0 ? 0 : 2);
-      const int kx = px ? 1 : (dx == 0 ? 0 : 2);
+    for (int p = 0; p < 4; ++p)
+      if (!((dy != 0 && (p >> 1) == 1) || (dx != 0 && (p & 1) == 1))) ph[np++] = p;
+#pragma unroll
+    for (int k = 0; k + 1 < np; k += 2) {
+      const int pa = ph[k], pb = ph[k + 1];
+      const int kya = (pa >> 1) ? 1 : (dy == 0 ? 0 : 2), kxa = (pa & 1) ? 1 : (dx == 0 ? 0 : 2);
+      const int kyb = (pb >> 1) ? 1 : (dy == 0 ? 0 : 2), kxb = (pb & 1) ? 1 : (dx == 0 ? 0 : 2);
 #pragma unroll
       for (int co = 0; co < 3; ++co) {
-        const float* wk = w + ((ky * 3 + kx) * 3 + co) * CIN;
+        const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
+        const float* wb = w + ((kyb * 3 + kxb) * 3 + co) * CIN;
+        f32x2 s2 = {acc[pa][co], acc[pb][co]};
 #pragma unroll
-        for (int c4 = 0; c4 < C4; ++c4) {
-          const f32x4 wv = *reinterpret_cast<const f32x4*>(wk + 4 * c4);
-          acc[ph][co] = fmaf(x[4 * c4], wv.x, acc[ph][co]);
-          acc[ph][co] = fmaf(x[4 * c4 + 1], wv.y, acc[ph][co]);
-          acc[ph][co] = fmaf(x[4 * c4 + 2], wv.z, acc[ph][co]);
-          acc[ph][co] = fmaf(x[4 * c4 + 3], wv.w, acc[ph][co]);
+        for (int ci = 0; ci < CIN; ++ci) {
+          const f32x2 xx = {x[ci], x[ci]};
+          const f32x2 ww = {wa[ci], wb[ci]};
+          s2 = __builtin_elementwise_fma(xx, ww, s2);
         }
+        acc[pa][co] = s2.x;
+        acc[pb][co] = s2.y;
+      }
+    }
+    if (np & 1) {
+      const int pa = ph[np - 1];
+      const int kya = (pa >> 1) ? 1 : (dy == 0 ? 0 : 2), kxa = (pa & 1) ? 1 : (dx == 0 ? 0 : 2);
+#pragma unroll
+      for (int co = 0; co < 3; ++co) {
+        const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) acc[pa][co] = fmaf(x[ci], wa[ci], acc[pa][co]);
       }
     }
   }
