@@ -141,3 +141,26 @@ def test_npz_round_trip(tmp_path):
     save_params(str(tmp_path / "w.npz"), p)
     q = load_params(str(tmp_path / "w"))
     assert set(p) == set(q) and all(np.array_equal(p[k], q[k]) for k in p)
+
+
+def test_bench_groups_fused_layer_pairs():
+    """bench.py's roofline grouping: a layer launched inside the previous one (kernel name
+    '') forms one group with it — FLOPs of both, the f32 intermediate excluded from bytes."""
+    import importlib.util
+    import os
+    import numpy as np
+    from tf_image_compression_amd.topology import layer_table, layer_work
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    L = len(layer_table(0))
+    kernels = [f"k{i}" for i in range(L)]
+    kernels[-1] = ""  # decode_0 inside decode_1's launch (dec10_kernel)
+    groups, rows = bench.kernel_groups(None, 0, 256, np.full(L, 0.01), kernels)
+    fused = [g for k, g in groups.items() if "fused" in k]
+    assert len(fused) == 1 and fused[0]["layers"] == ["decode_1", "decode_0"] and fused[0]["launches"] == 1
+    work = layer_work(0, 256)
+    (l1, f1, b1, ho1), (l0, f0, b0, _) = work[-2], work[-1]
+    assert fused[0]["flops"] == f1 + f0
+    assert fused[0]["bytes"] == b1 + b0 - 2 * ho1 * ho1 * l1.cout * 4 == 64 * 64 * 32 * 4 + 256 * 256 * 3
+    assert sum(g["launches"] for g in groups.values()) == L - 1
