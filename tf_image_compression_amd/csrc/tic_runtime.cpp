@@ -909,6 +909,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
   h->s1_form = default_s1_form();
+  if (const char* f = getenv("TIC_FUSE01")) h->fuse01 = atoi(f) != 0;
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   else h->fuse_tail = kFuseTailDefault;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
