@@ -44,8 +44,9 @@ def parse():
     ap.add_argument("--tune-step", type=int, default=1,
                     help="rounds of in-situ (whole dual-lane step) tuning after the per-layer autotune; 0 = off")
     ap.add_argument("--graph", action="store_true", help="replay the launch sequence as a HIP graph (opt-in)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
-                    help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic; default: the "
+                         "committed tools/pmc/traffic_r01_v8*.json of the model")
     ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
     ap.add_argument("--workload", choices=["patches", "image4k"], default="patches",
                     help="patches: BASELINE configs[1]/[2] (default); image4k: configs[4], whole "
@@ -56,6 +57,8 @@ def parse():
     args = ap.parse_args()
     if args.workload == "image4k" and "--model" not in sys.argv:
         args.model = 3
+    if args.traffic is None:
+        args.traffic = os.path.join(ROOT, "tools", "pmc", "traffic_r01_v8%s.json" % ("" if args.model == 0 else "_model3"))
     return args
 
 
@@ -444,7 +447,7 @@ def main_image(args):
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
     # HBM bytes per launch from the PMC summaries (tools/pmc_round.sh); the PMC runs launch
     # 32 (configs[1]) or 128 (configs[2]) patches per kernel, this workload lb: scaled
-    for path in (args.traffic, os.path.join(ROOT, "profiles", "traffic_r01_model3.json")):
+    for path in (args.traffic, os.path.join(ROOT, "tools", "pmc", "traffic_r01_v8_model3.json")):
         if roof["traffic"] is None and os.path.exists(path):
             tr = json.load(open(path))
             ents = [tr[k] for k in dom_kernels if k in tr]
