@@ -26,6 +26,9 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA / vector peak (spec)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
+# Winograd F(2x2,3x3): 16 transform points per 2x2 output tile instead of 4 x 9 taps, so
+# the minimal-form FLOP count of a stride-1 layer run in that form is 16/36 of the direct one
+WINO_FRAC = 16.0 / 36.0
 
 
 def parse():
@@ -46,7 +49,12 @@ def parse():
     ap.add_argument("--graph", action="store_true", help="replay the launch sequence as a HIP graph (opt-in)")
     ap.add_argument("--traffic", default=None,
                     help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic; default: the "
-                         "committed tools/pmc/traffic_r01_v8*.json of the model")
+                         "committed tools/pmc/traffic_model<N>.json, used only if its source stamp "
+                         "matches these kernel sources and its configuration matches this run")
+    ap.add_argument("--pmc-plan", default=None,
+                    help="PMC mode (tools/pmc_box.sh): tune exactly as the bench does, then run --steps "
+                         "steps on ONE lane at the per-lane batch (deterministic dispatch order), write "
+                         "the launch plan of one step to this path, print nothing else")
     ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
     ap.add_argument("--workload", choices=["patches", "image4k"], default="patches",
                     help="patches: BASELINE configs[1]/[2] (default); image4k: configs[4], whole "
@@ -58,7 +66,9 @@ def parse():
     if args.workload == "image4k" and "--model" not in sys.argv:
         args.model = 3
     if args.traffic is None:
-        args.traffic = os.path.join(ROOT, "tools", "pmc", "traffic_r01_v8%s.json" % ("" if args.model == 0 else "_model3"))
+        # committed PMC summaries exist per model (tools/pmc); none for models 1/2 -> None
+        name = {0: "traffic_model0.json", 3: "traffic_model3.json"}.get(args.model)
+        args.traffic = os.path.join(ROOT, "tools", "pmc", name) if name else ""
     return args
 
 
@@ -73,6 +83,9 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
     n_enc = sum(1 for lay, *_ in work if lay.stage == "enc")
     groups = {}
     rows = []
+    if kernels is not None:  # Winograd-form layers: count the FLOPs of the form that runs
+        work = [(lay, f * WINO_FRAC if "wino" in kernels[i] else f, b, ho)
+                for i, (lay, f, b, ho) in enumerate(work)]
     for i, (lay, flops, nbytes, ho) in enumerate(work):
         role = "rgb_in" if i == 0 else ("rgb_out" if i == L - 1 else
                                         ("quant" if (model_id != RMBE_ID and i == n_enc - 1) else
@@ -129,45 +142,131 @@ def step_roofline(rows, batch, step_ms):
 
 
 def winograd_note(roof, kernels, flops, ms):
-    """Winograd F(2x2,3x3) kernels execute 16/36 of the direct form's MACs on the matrix
-    cores: `achieved` stays the algorithmic (direct-form) FLOP rate, `executed` is what the
-    MFMA pipes actually ran, the fraction of peak that measures kernel quality."""
+    """A Winograd F(2x2,3x3) group's FLOPs are already the minimal-form count (16/36 of the
+    direct form: kernel_groups), so `achieved`/`frac` are what the matrix cores ran and
+    frac <= 1; the direct-form equivalent rate is reported beside it."""
     if kernels and all("wino" in k for k in kernels):
-        ex = flops * 16.0 / 36.0 / (ms * 1e-3) / 1e12
-        roof["executed"] = {"form": "winograd F(2x2,3x3): 16/36 of the direct MACs",
-                            "mfma_tflops": round(ex, 2), "frac": round(ex / PEAK_FP32_TFLOPS, 4)}
+        roof["flop_form"] = "winograd F(2x2,3x3) minimal form: 16/36 of the direct-form FLOPs"
+        roof["direct_equiv_tflops"] = round(flops / WINO_FRAC / (ms * 1e-3) / 1e12, 2)
 
 
-def cpu_baseline(model_id, P, params, mean, std, target_s):
-    """The oracle (numpy, float32 GEMMs on OpenBLAS) timed on this box's host cores on a
-    bounded sample of the same workload; the reference's TF-CPU path cannot run here."""
+def launch_units(layer_names, kernels, names):
+    """Launch units of a kernel group: a layer, or 'a+b' where layer b ran inside layer a's
+    launch (kernel name '' = fused into the previous layer)."""
+    units = []
+    for nm in layer_names:
+        i = names[nm]
+        if kernels[i] == "":
+            continue
+        j = i + 1
+        unit = [nm]
+        inv = {v: k for k, v in names.items()}
+        while j < len(kernels) and kernels[j] == "":
+            unit.append(inv[j])
+            j += 1
+        units.append("+".join(unit))
+    return units
+
+
+def pmc_traffic(path, units, cfg):
+    """roofline.traffic: HBM bytes per launch of the dominant kernel group from a PMC summary
+    written by tools/pmc_summary.py (separate FETCH_SIZE / WRITE_SIZE passes of this same
+    bench under rocprofv3, gfx950 corrections), keyed by launch unit.  Used only when the
+    summary's source stamp equals these kernel sources and its model / patch / per-launch
+    batch equal this run's; otherwise traffic is null and the reason is given."""
+    from tf_image_compression_amd._lib import source_digest
+    out = {"traffic": None, "traffic_source": None}
+    if not path or not os.path.exists(path):
+        out["traffic_note"] = "no PMC summary for this model"
+        return out
+    tr = json.load(open(path))
+    meta = tr.get("_meta", {})
+    rel = os.path.relpath(path, ROOT)
+    if meta.get("source_sha256") != source_digest():
+        out["traffic_note"] = f"{rel} was measured on other kernel sources (stamp mismatch): not used"
+        return out
+    for k, v in cfg.items():
+        if meta.get(k) != v:
+            out["traffic_note"] = f"{rel} was measured at {k}={meta.get(k)}, this run {k}={v}: not used"
+            return out
+    ents = [tr["units"][u] for u in units if u in tr.get("units", {})]
+    if not ents:
+        out["traffic_note"] = f"{rel} has no entry for {units}"
+        return out
+    out["traffic"] = round(float(np.mean([e["bytes"] for e in ents])))
+    out["traffic_source"] = rel
+    out["traffic_read_write"] = [round(float(np.mean([e["read_bytes"] for e in ents]))),
+                                 round(float(np.mean([e["write_bytes"] for e in ents])))]
+    return out
+
+
+def host_cpu_info():
+    """CPUs this process may run on (affinity and cgroup quota), and the CPU model."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    info["model"] = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                info["model"] = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = info["affinity"] or 1
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    info["usable"] = usable
+    return info
+
+
+def cpu_baseline(model_id, P, params, mean, std, batch, target_s):
+    """The oracle in float32 (im2col + OpenBLAS SGEMM on every CPU this job may use) timed
+    on the GPU box's host on the same workload: one warm-up run, then the median of >= 5
+    timed runs of encode + decode of `batch` patches.  The reference's
+    TF-CPU path cannot run here (TF-1.x absent), so this is a disclosed stand-in."""
     from oracle import tic_oracle as o
     try:
         from threadpoolctl import threadpool_limits
     except Exception:  # pragma: no cover
         threadpool_limits = None
-    cores = min(16, os.cpu_count() or 1)
-    n = 8
+    cpu = host_cpu_info()
+    cores = cpu["usable"]
+    n = batch
     x = np.random.default_rng(99).integers(0, 256, (n, P, P, 3), dtype=np.uint8)
     ctx = threadpool_limits(limits=cores) if threadpool_limits else None
     times = []
     try:
-        t_begin = time.perf_counter()
-        while True:
-            t0 = time.perf_counter()
+        def run():
             _, idx = o.encoder(params, mean, std, x, P, 2, model_id, acc=np.float32)
             o.decoder(params, mean, std, idx, 2, model_id, acc=np.float32)
+        t_begin = time.perf_counter()
+        run()  # warm-up
+        while True:
+            t0 = time.perf_counter()
+            run()
             times.append(time.perf_counter() - t0)
-            if time.perf_counter() - t_begin > target_s and len(times) >= 3:
+            if len(times) >= 5 and time.perf_counter() - t_begin > target_s:
                 break
     finally:
-        if ctx is not None:
-            ctx.unregister() if hasattr(ctx, "unregister") else None
+        if ctx is not None and hasattr(ctx, "unregister"):
+            ctx.unregister()
     med = float(np.median(times))
     return {"value": round(n * P * P / med / 1e6, 3), "unit": "MPix/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/tic_oracle.py float32 (OpenBLAS {cores} threads), model_{model_id} "
-                      f"{n} x {P}x{P} patches encode+decode, median of {len(times)} runs "
-                      f"({sum(times):.1f} s total)"}
+            "host": cpu,
+            "sample": f"oracle/tic_oracle.py float32 (im2col + OpenBLAS SGEMM, {cores} threads = every CPU "
+                      f"this job may use), model_{model_id} batch {n} x {P}x{P} patches encode+decode, "
+                      f"1 warm-up + median of {len(times)} runs ({sum(times):.1f} s timed)"}
 
 
 def parity_probe(codec, model_id, P, params, mean, std):
@@ -222,6 +321,8 @@ def main():
         codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice, outside the timed region
         if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
             codec.autotune_step(d_in, B, rounds=args.tune_step, reps=5)
+    if args.pmc_plan:
+        return pmc_steady(args, codec, d_in, d_idx, d_rgb, lane_b, M, P)
     for _ in range(args.warmup):
         codec.codec_device(d_in, B, d_idx, d_rgb)
     codec.synchronize()
@@ -257,14 +358,8 @@ def main():
     # (tools/pmc_box.sh + tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
     names = {lay.name: i for i, lay in enumerate(layer_table(M))}
     dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
-    roof["traffic"] = None
-    roof["traffic_source"] = None
-    if os.path.exists(args.traffic):
-        tr = json.load(open(args.traffic))
-        ents = [tr[k] for k in dom_kernels if k in tr]
-        if ents:
-            roof["traffic"] = round(float(np.mean([e["bytes"] for e in ents])))
-            roof["traffic_source"] = os.path.relpath(args.traffic, ROOT)
+    roof.update(pmc_traffic(args.traffic, launch_units(groups[dom_key]["layers"], kernels, names),
+                            {"model": M, "patch": P, "lane_batch": lane_b}))
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
     roof["kernel"] = "+".join(groups[dom_key]["layers"])
     roof["kernel_instance"] = dom_kernels
@@ -309,10 +404,39 @@ def main():
             pass
         out["parity"] = parity_probe(codec, M, P, params, SYNTH_MEAN, SYNTH_STD)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(M, P, params, SYNTH_MEAN, SYNTH_STD, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(M, P, params, SYNTH_MEAN, SYNTH_STD,
+                                               B if M in (0, 1) else min(B, 8), args.cpu_seconds)
             out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     comm.close()
+    codec.close()
+
+
+def pmc_steady(args, codec, d_in, d_idx, d_rgb, lane_b, M, P):
+    """--pmc-plan: after the bench's own tuning, run --steps steps on ONE lane at the
+    per-lane batch (the tuned choices are keyed by that batch, so every launch is the
+    bench's), with the launch plan of one step written for tools/pmc_summary.py."""
+    from tf_image_compression_amd._lib import source_digest, lib_digest
+    from tf_image_compression_amd.topology import layer_table
+    kernels = codec.layer_kernels(lane_b)
+    names = [lay.name for lay in layer_table(M)]
+    plan = []
+    for i, k in enumerate(kernels):
+        if k == "":
+            plan[-1]["unit"] += "+" + names[i]
+            continue
+        plan.append({"unit": names[i], "kernel": k})
+    codec.set_option("streams", 1)
+    for _ in range(args.warmup):
+        codec.codec_device(d_in, lane_b, d_idx, d_rgb)
+    codec.synchronize()
+    for _ in range(args.steps):
+        codec.codec_device(d_in, lane_b, d_idx, d_rgb)
+    codec.synchronize()
+    meta = {"model": M, "patch": P, "lane_batch": lane_b, "steps": args.steps, "source_sha256": source_digest(),
+            "libtic_sha256": lib_digest(), "streams_in_bench": args.streams}
+    os.makedirs(os.path.dirname(os.path.abspath(args.pmc_plan)), exist_ok=True)
+    json.dump({"_meta": meta, "plan": plan}, open(args.pmc_plan, "w"), indent=1)
     codec.close()
 
 
@@ -325,7 +449,8 @@ def cpu_baseline_image(model_id, P, params, mean, std, rparams, H, W, target_s):
         from threadpoolctl import threadpool_limits
     except Exception:  # pragma: no cover
         threadpool_limits = None
-    cores = min(16, os.cpu_count() or 1)
+    cpu = host_cpu_info()
+    cores = cpu["usable"]
     n_p, n_w = 2, 4
     r = np.random.default_rng(98)
     x = r.integers(0, 256, (n_p, P, P, 3), dtype=np.uint8)
@@ -351,7 +476,7 @@ def cpu_baseline_image(model_id, P, params, mean, std, rparams, H, W, target_s):
     n_win = (H // 128) * ((W - 64) // 128) + ((H - 64) // 128) * (W // 128)
     t_img = float(np.median(tp)) / n_p * hn * wn + float(np.median(tw)) / n_w * n_win
     return {"value": round(H * W / t_img / 1e6, 4), "unit": "MPix/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/tic_oracle.py float32 (OpenBLAS {cores} threads): model_{model_id} "
+            "host": cpu, "sample": f"oracle/tic_oracle.py float32 (OpenBLAS {cores} threads): model_{model_id} "
                       f"{n_p} x {P}x{P} patches encode+decode and rmbe {n_w} x 128x128 windows, median of "
                       f"{len(tp)} runs, extrapolated to {hn * wn} patches + {n_win} windows of one "
                       f"{W}x{H} image"}
@@ -437,25 +562,15 @@ def main_image(args):
     dom_key = max(per_img, key=lambda k: per_img[k][0]["ms"] * per_img[k][2] / per_img[k][1])
     g, lb, _ = per_img[dom_key]
     roof, dom_ms, dom_flops, _ = roofline_of(g, lb)
-    roof["traffic"] = None
-    roof["traffic_source"] = None
     from tf_image_compression_amd.topology import layer_table
     net, net_id = (post, RMBE_ID) if dom_key[0] == "rmbe" else (codec, M)
     kern = net.layer_kernels(lb)
     idx = {lay.name: i for i, lay in enumerate(layer_table(net_id))}
     dom_kernels = sorted({kern[idx[nm]] for nm in g["layers"]} - {""})
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
-    # HBM bytes per launch from the PMC summaries (tools/pmc_round.sh); the PMC runs launch
-    # 32 (configs[1]) or 128 (configs[2]) patches per kernel, this workload lb: scaled
-    for path in (args.traffic, os.path.join(ROOT, "tools", "pmc", "traffic_r01_v8_model3.json")):
-        if roof["traffic"] is None and os.path.exists(path):
-            tr = json.load(open(path))
-            ents = [tr[k] for k in dom_kernels if k in tr]
-            if ents:
-                pmc_lane = 128 if "model3" in path else 32  # patches per launch in the PMC run
-                roof["traffic"] = round(float(np.mean([e["bytes"] for e in ents])) * lb / pmc_lane)
-                roof["traffic_source"] = os.path.relpath(path, ROOT)
-                roof["traffic_note"] = f"PMC bytes per launch at {pmc_lane} patches, scaled to {lb}"
+    # HBM bytes per launch: only from a PMC summary of this exact configuration
+    roof.update(pmc_traffic(args.traffic if dom_key[0] != "rmbe" else "", launch_units(g["layers"], kern, idx),
+                            {"model": net_id, "patch": P if dom_key[0] != "rmbe" else 128, "lane_batch": lb}))
     roof["kernel_instance"] = dom_kernels
     roof["kernel"] = ("rmbe:" if dom_key[0] == "rmbe" else f"model_{M}:") + "+".join(g["layers"])
     roof["ms_per_launch"] = round(dom_ms, 5)

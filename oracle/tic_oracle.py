@@ -66,7 +66,7 @@ _M0_DEC = [
     ("decode_1", "convT", 32, 32, "relu"),
     ("decode_0", "convT", 32, 3, "identity"),
 ]
-# model_1/model.py: as model_0 but widths 16 at the ends (:52 filters=16, :198 filters=16)
+# model_1/model.py: as model_0 but widths 16 at the ends (:52 filters=16, :226 filters=16)
 _M1_ENC = [
     ("encode_0", "conv_s2", 3, 16, "relu"),
     ("encode_1", "conv_s2", 16, 32, "relu"),

@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from conftest import structured_patches
+from gpu_checks import check_codec as _check_codec, codec_mean, codec_std  # noqa: F401
 from oracle import tic_oracle as o
 
 pytestmark = pytest.mark.gpu
@@ -114,40 +115,6 @@ def test_conv3x3_layer(lib_codec, kind, cin, cout, act, res, H, W):
         assert err <= 3e-5 * scale, (tile, err, scale)
         # every tiling runs the same per-output fma order: results are bit-identical
         assert np.array_equal(got, outs[0][1]), tile
-
-
-def _check_codec(codec, params, model_id, P, patches, Q=2):
-    idx, pre = codec.encode(patches, return_preact=True)
-    ref_pre, ref_idx = o.encoder(params, codec_mean(), codec_std(), patches, P, Q, model_id)
-    scale = max(1.0, float(np.max(np.abs(ref_pre))))
-    assert pre.shape == ref_pre.shape and idx.shape == ref_idx.shape
-    assert float(np.max(np.abs(pre - ref_pre))) <= 1e-4 * scale
-    margin = o.decision_margin(ref_pre, Q)
-    safe = margin > 1e-5 * scale
-    mism = int(np.count_nonzero((idx != ref_idx) & safe))
-    assert mism == 0, f"{mism} symbol mismatches outside the tie band"
-    # decoder on the GPU's own symbols, oracle on the same symbols
-    rgb, f = codec.decode(idx, return_float=True)
-    ref_f, ref_u8 = o.decoder(params, codec_mean(), codec_std(), idx, Q, model_id)
-    assert float(np.max(np.abs(f - ref_f))) <= 1e-2
-    du = np.abs(rgb.astype(np.int16) - ref_u8.astype(np.int16))
-    assert int(du.max()) <= 1
-    edge = np.abs((ref_f - np.floor(ref_f)) - 0.5) < 1e-2
-    assert int(np.count_nonzero((du > 0) & ~edge)) == 0
-    p_gpu = o.dataset_psnr([(patches[i], rgb[i]) for i in range(len(patches))])
-    p_ref = o.dataset_psnr([(patches[i], ref_u8[i]) for i in range(len(patches))])
-    assert abs(p_gpu - p_ref) <= 0.02, (p_gpu, p_ref)
-    return idx, rgb
-
-
-def codec_mean():
-    from tf_image_compression_amd.weights import SYNTH_MEAN
-    return SYNTH_MEAN
-
-
-def codec_std():
-    from tf_image_compression_amd.weights import SYNTH_STD
-    return SYNTH_STD
 
 
 # Winograd F(2x2,3x3) tilings of the stride-1 layers: (th = 2 TTY, nsplit, NN)

@@ -127,6 +127,31 @@ def test_prob_to_cum_freq_properties():
     assert c0 == c1
 
 
+def _greedy_reference(prob, resolution):
+    """The published allocation of the range_coder package, written as the plain loop:
+    `resolution` times, freq[nanargmax(prob / freq)] += 1."""
+    prob = np.asarray(prob, dtype=np.float64)
+    freq = np.zeros(prob.size, dtype=np.int64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for _ in range(resolution):
+            freq[np.nanargmax(prob / freq)] += 1
+    return [0] + np.cumsum(freq).tolist()
+
+
+@pytest.mark.parametrize("seed,n,res", [(0, 2, 4096), (1, 3, 8), (2, 50, 1024), (3, 256, 4096), (4, 7, 7),
+                                        (5, 16, 100)])
+def test_prob_to_cum_freq_matches_greedy_loop(seed, n, res):
+    rs = np.random.RandomState(seed)
+    p = rs.dirichlet([0.3] * n)
+    p[rs.rand(n) < 0.2] = 0.0
+    if p.sum() == 0:
+        p[0] = 1.0
+    assert prob_to_cum_freq(p, res) == _greedy_reference(p, res)
+    # the reference CLI's construction (encode.py:81-86) too
+    m = p * 4096 + 1
+    assert symbol_table(p, 4096) == _greedy_reference(m / m.sum(), 4096)
+
+
 def test_prob_to_cum_freq_zero_prob():
     c1 = prob_to_cum_freq([0.5, 0.25, 0.25], resolution=8)
     c0 = prob_to_cum_freq([0.5, 0., 0.25, 0.25, 0., 0.], resolution=8)

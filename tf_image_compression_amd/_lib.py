@@ -116,6 +116,32 @@ def check(rc: int, what: str = "") -> int:
     return rc
 
 
+def source_digest() -> str:
+    """SHA-256 over the kernel / runtime sources and the build flags: the stamp that ties a
+    PMC summary (tools/pmc_summary.py) to the code whose kernels it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(_HERE, "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".h", ".hip", ".cpp")):
+            h.update(name.encode())
+            with open(os.path.join(csrc, name), "rb") as f:
+                h.update(f.read())
+    mk = os.path.join(os.path.dirname(_HERE), "Makefile")
+    if os.path.exists(mk):
+        with open(mk, "rb") as f:
+            h.update(b"".join(ln for ln in f.read().splitlines(True) if ln.startswith(b"HIPFLAGS")))
+    return h.hexdigest()
+
+
+def lib_digest() -> str | None:
+    import hashlib
+    if not os.path.exists(LIB_PATH):
+        return None
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def ptr(arr, ctype):
     """Pointer to a C-contiguous numpy array's data (or NULL for None)."""
     if arr is None:

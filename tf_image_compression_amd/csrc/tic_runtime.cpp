@@ -44,6 +44,28 @@ int fail(int code, const char* fmt, ...) {
                   __LINE__);                                                                \
   } while (0)
 
+// Scoped timing event / device scratch: released on every exit path (HIP_TRY returns early).
+struct Event {
+  hipEvent_t e = nullptr;
+  Event() = default;
+  Event(const Event&) = delete;
+  Event& operator=(const Event&) = delete;
+  ~Event() {
+    if (e) (void)hipEventDestroy(e);
+  }
+  hipError_t create() { return hipEventCreate(&e); }
+};
+struct Scratch {
+  void* p = nullptr;
+  Scratch() = default;
+  Scratch(const Scratch&) = delete;
+  Scratch& operator=(const Scratch&) = delete;
+  ~Scratch() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes); }
+};
+
 enum { K_S1 = 0, K_S2 = 1, K_T2 = 2 };
 
 struct LayerDef {
@@ -381,8 +403,16 @@ int ensure(void** p, size_t* have, size_t need) {
   return TIC_OK;
 }
 
+void clear_graphs(tic_handle* h) {
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
+}
+
+// Grow a lane's workspace.  Captured graphs hold the old workspace pointers, so every
+// reallocation drops them (they are re-captured on their next use).
 int ensure_ws(tic_handle* h, Lane& ln, int n) {
   if (ln.ws_batch >= n) return TIC_OK;
+  clear_graphs(h);
   for (auto& b : ln.ws) {
     if (b) (void)hipFree(b);
     b = nullptr;
@@ -391,11 +421,6 @@ int ensure_ws(tic_handle* h, Lane& ln, int n) {
   for (auto& b : ln.ws) HIP_TRY(hipMalloc((void**)&b, h->act_elems * (size_t)n * sizeof(float)));
   ln.ws_batch = n;
   return TIC_OK;
-}
-
-void clear_graphs(tic_handle* h) {
-  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-  h->graphs.clear();
 }
 
 int check_launch() {
@@ -408,27 +433,25 @@ int check_launch() {
 int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(int)>& launch, int* best,
                   const char* label = "", int n = 0) {
   static const bool log = getenv("TIC_TUNE_LOG") != nullptr;
-  hipEvent_t t0, t1;
-  HIP_TRY(hipEventCreate(&t0));
-  HIP_TRY(hipEventCreate(&t1));
+  Event t0, t1;
+  HIP_TRY(t0.create());
+  HIP_TRY(t1.create());
   float best_ms = 1e30f;
   *best = -1;
   for (int v = 0; v < nvar; ++v) {
     if (!launch(v)) continue;
-    HIP_TRY(hipEventRecord(t0, st));
+    HIP_TRY(hipEventRecord(t0.e, st));
     for (int r = 0; r < reps; ++r) launch(v);
-    HIP_TRY(hipEventRecord(t1, st));
-    HIP_TRY(hipEventSynchronize(t1));
+    HIP_TRY(hipEventRecord(t1.e, st));
+    HIP_TRY(hipEventSynchronize(t1.e));
     float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+    HIP_TRY(hipEventElapsedTime(&ms, t0.e, t1.e));
     if (log) fprintf(stderr, "tune %-22s n=%d variant %d : %.2f us\n", label, n, v, 1e3f * ms / reps);
     if (ms < best_ms) {
       best_ms = ms;
       *best = v;
     }
   }
-  (void)hipEventDestroy(t0);
-  (void)hipEventDestroy(t1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(TIC_EHIP, "tuning launch failed: %s", hipGetErrorString(e));
   if (*best < 0) return fail(TIC_EUNSUPPORTED, "no launchable variant");
@@ -681,20 +704,20 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       if (h->tune_reps > 0 && it == lay.tuned.end()) {
         // time every compiled tiling on the live buffers (re-launching is idempotent)
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, layer_form(h, lay));
-        hipEvent_t t0, t1;
-        HIP_TRY(hipEventCreate(&t0));
-        HIP_TRY(hipEventCreate(&t1));
+        Event t0, t1;
+        HIP_TRY(t0.create());
+        HIP_TRY(t1.create());
         float best_ms = 1e30f;
         const bool log = getenv("TIC_TUNE_LOG") != nullptr;
         for (const tic::ConvEntry* c : cands) {
           a.wp = conv_weights(lay, c);
           c->fn(a, n, st);  // warm
-          HIP_TRY(hipEventRecord(t0, st));
+          HIP_TRY(hipEventRecord(t0.e, st));
           for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, st);
-          HIP_TRY(hipEventRecord(t1, st));
-          HIP_TRY(hipEventSynchronize(t1));
+          HIP_TRY(hipEventRecord(t1.e, st));
+          HIP_TRY(hipEventSynchronize(t1.e));
           float ms = 0.f;
-          HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
+          HIP_TRY(hipEventElapsedTime(&ms, t0.e, t1.e));
           if (log)
             fprintf(stderr, "tune %-22s n=%d th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), n, c->th, c->nsplit,
                     c->wlds, 1e3f * ms / h->tune_reps);
@@ -703,8 +726,6 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
             e = c;
           }
         }
-        (void)hipEventDestroy(t0);
-        (void)hipEventDestroy(t1);
         int rc = check_launch();
         if (rc) return rc;
         lay.tuned[tkey(h, lay, n)] = e;
@@ -1294,14 +1315,19 @@ int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float*
   if (!d_in || n <= 0 || iters <= 0 || !ms_out) return fail(TIC_EINVAL, "bad arguments");
   if (n > h->chunk) return fail(TIC_EINVAL, "profile n %d exceeds chunk %d", n, h->chunk);
   const int L = (int)h->layers.size();
+  std::vector<Event> evs(2 * L);
   std::vector<hipEvent_t> ev(2 * L);
-  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  for (int i = 0; i < 2 * L; ++i) {
+    HIP_TRY(evs[i].create());
+    ev[i] = evs[i].e;
+  }
   std::vector<double> acc(L, 0.0);
-  void *d_idx = nullptr, *d_out = nullptr;
   const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
   const size_t px = (size_t)n * h->P * h->P * 3;
-  HIP_TRY(hipMalloc(&d_idx, std::max<size_t>(ce, 16)));
-  HIP_TRY(hipMalloc(&d_out, px * (h->rmbe() ? 4 : 1)));
+  Scratch s_idx, s_out;
+  HIP_TRY(s_idx.alloc(std::max<size_t>(ce, 16)));
+  HIP_TRY(s_out.alloc(px * (h->rmbe() ? 4 : 1)));
+  void *d_idx = s_idx.p, *d_out = s_out.p;
   for (int it = 0; it < iters && rc == TIC_OK; ++it) {
     if (h->rmbe()) {
       rc = rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{ev.data()});
@@ -1320,9 +1346,6 @@ int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float*
     }
   }
   for (int i = 0; i < L; ++i) ms_out[i] = (float)(acc[i] / iters);
-  for (auto& e : ev) (void)hipEventDestroy(e);
-  (void)hipFree(d_idx);
-  (void)hipFree(d_out);
   return rc;
 }
 
@@ -1337,11 +1360,12 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
     l.tuned_var.erase(-n);
   }
   clear_graphs(h);
-  void *d_idx = nullptr, *d_out = nullptr;
   const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
   const size_t px = (size_t)n * h->P * h->P * 3;
-  HIP_TRY(hipMalloc(&d_idx, std::max<size_t>(ce, 16)));
-  HIP_TRY(hipMalloc(&d_out, px * (h->rmbe() ? 4 : 1)));
+  Scratch s_idx, s_out;
+  HIP_TRY(s_idx.alloc(std::max<size_t>(ce, 16)));
+  HIP_TRY(s_out.alloc(px * (h->rmbe() ? 4 : 1)));
+  void *d_idx = s_idx.p, *d_out = s_out.p;
   h->tune_reps = reps;
   if (h->rmbe()) {
     rc = rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr});
@@ -1351,8 +1375,6 @@ int tic_autotune(tic_handle* h, const void* d_in, int n, int reps) {
   }
   h->tune_reps = 0;
   hipError_t e = hipStreamSynchronize(h->stream);
-  (void)hipFree(d_idx);
-  (void)hipFree(d_out);
   if (rc) return rc;
   if (e != hipSuccess) return fail(TIC_EHIP, "autotune sync: %s", hipGetErrorString(e));
   return TIC_OK;
@@ -1390,14 +1412,16 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     }
   }
   clear_graphs(h);
-  void *d_idx = nullptr, *d_out = nullptr;
   const size_t ce = h->rmbe() ? 0 : (size_t)n * code_elems(h);
   const size_t px = (size_t)n * h->P * h->P * 3;
-  HIP_TRY(hipMalloc(&d_idx, std::max<size_t>(ce, 16)));
-  HIP_TRY(hipMalloc(&d_out, px * (h->rmbe() ? 4 : 1)));
-  hipEvent_t t0 = nullptr, t1 = nullptr;
-  HIP_TRY(hipEventCreate(&t0));
-  HIP_TRY(hipEventCreate(&t1));
+  Scratch s_idx, s_out;
+  HIP_TRY(s_idx.alloc(std::max<size_t>(ce, 16)));
+  HIP_TRY(s_out.alloc(px * (h->rmbe() ? 4 : 1)));
+  void *d_idx = s_idx.p, *d_out = s_out.p;
+  Event ev0, ev1;
+  HIP_TRY(ev0.create());
+  HIP_TRY(ev1.create());
+  hipEvent_t t0 = ev0.e, t1 = ev1.e;
   auto step = [&]() {
     return h->rmbe() ? rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr})
                      : codec_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, (uint8_t*)d_out);
@@ -1503,10 +1527,6 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     if (log && !rc) fprintf(stderr, "tune-step n=%d after round %d: %.2f us\n", n, round + 1, 1e3f * cur);
   }
   hipError_t e = hipStreamSynchronize(h->stream);
-  (void)hipEventDestroy(t0);
-  (void)hipEventDestroy(t1);
-  (void)hipFree(d_idx);
-  (void)hipFree(d_out);
   if (rc) return rc;
   if (e != hipSuccess) return fail(TIC_EHIP, "autotune_step sync: %s", hipGetErrorString(e));
   return TIC_OK;
@@ -1620,9 +1640,10 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   std::vector<float> wp;
   if (e->wlds == 4) pack_wino(w_host, cin, cout, &wp);
   else pack_generic(w_host, kind, cin, cout, &wp);
-  float *d_w = nullptr, *d_b = nullptr;
-  HIP_TRY(hipMalloc((void**)&d_w, wp.size() * 4));
-  HIP_TRY(hipMalloc((void**)&d_b, (size_t)cout * 4));
+  Scratch s_w, s_b;
+  HIP_TRY(s_w.alloc(wp.size() * 4));
+  HIP_TRY(s_b.alloc((size_t)cout * 4));
+  float *d_w = (float*)s_w.p, *d_b = (float*)s_b.p;
   HIP_TRY(hipMemcpy(d_w, wp.data(), wp.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_b, b_host, (size_t)cout * 4, hipMemcpyHostToDevice));
   tic::ConvArgs a{};
@@ -1642,8 +1663,6 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   e->fn(a, n, h->stream);
   int rc = check_launch();
   hipError_t se = hipStreamSynchronize(h->stream);
-  (void)hipFree(d_w);
-  (void)hipFree(d_b);
   if (rc) return rc;
   if (se != hipSuccess) return fail(TIC_EHIP, "conv3x3 sync: %s", hipGetErrorString(se));
   return TIC_OK;

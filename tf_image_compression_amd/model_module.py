@@ -48,17 +48,38 @@ class ModelModule:
         return self._codecs[key]
 
     def encoder(self, input, patch_size, quan_scale):
+        """The reference feeds skimage's uint8 pixels cast to float32 (encode.py:154-157,
+        model_0/model.py:39-44).  The device path reads uint8, so float input is accepted
+        only when every value is an integer in [0, 255] (exactly what the reference sees);
+        anything else raises instead of being silently rounded."""
         x = np.asarray(input)
         if x.dtype != np.uint8:
-            x = np.clip(np.rint(x), 0, 255).astype(np.uint8)
+            if not np.issubdtype(x.dtype, np.number):
+                raise ValueError(f"encoder input must be numeric, got {x.dtype}")
+            xf = x.astype(np.float64)
+            if not np.all(np.isfinite(xf)) or np.any(xf != np.rint(xf)) or np.any(xf < 0) or np.any(xf > 255):
+                raise ValueError("encoder input must hold integer pixel values in [0, 255] "
+                                 "(the device path reads uint8 pixels)")
+            x = xf.astype(np.uint8)
+        if x.size % (patch_size * patch_size * 3):
+            raise ValueError(f"input of {x.size} values is not a whole number of {patch_size}x{patch_size}x3 patches")
         return self.codec(patch_size, quan_scale).encode(x.reshape(-1, patch_size, patch_size, 3))
 
     def _patch_for(self, input, quan_scale):
+        """The decoder graph takes [N, h, w, C] and returns [N, P, P, 3] (decode.py:159-167):
+        P follows from the code's spatial size and the model's stride-2 layers."""
+        shape = tuple(np.shape(input)[1:])
+        if len(shape) != 3 or shape[0] != shape[1]:
+            raise ValueError(f"decoder input must be [N, h, h, C], got {np.shape(input)}")
         for (p, q), c in self._codecs.items():
-            if q == quan_scale and tuple(c.code_shape) == tuple(np.shape(input)[1:]):
+            if q == quan_scale and tuple(c.code_shape) == shape:
                 return c
-        from .config import load_config
-        return self.codec(load_config(self.model_id)["patch_size"], quan_scale)
+        from .topology import bottleneck_shape, layer_table
+        n_s2 = sum(1 for lay in layer_table(self.model_id) if lay.stage == "enc" and lay.kind == "conv_s2")
+        P = shape[0] << n_s2
+        if tuple(bottleneck_shape(self.model_id, P)) != shape:
+            raise ValueError(f"model_{self.model_id}: no patch size produces a code of shape {shape}")
+        return self.codec(P, quan_scale)
 
     def decoder(self, input, quan_scale):
         _, f = self._patch_for(input, quan_scale).decode(np.asarray(input), return_float=True)

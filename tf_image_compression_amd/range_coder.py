@@ -122,36 +122,34 @@ class RangeDecoder:
 
 
 def prob_to_cum_freq(prob, resolution=1024):
-    """Probability vector -> cumulative frequency table [0, ..., resolution] in which every
-    non-zero probability gets a non-zero frequency and zero probabilities get none
-    (properties pinned by other/test_range_coder.py:186-229).  Frequencies are
-    floor(p * resolution), raised to 1 for every non-zero p; missing counts go to the
-    largest fractional remainders (ties to the lower index), surplus counts are taken from
-    the entries rounded up the most.  The package's exact rounding is unvendored."""
+    """Probability vector -> cumulative frequency table [0, ..., resolution].
+
+    The budget is handed out one count at a time, each to the entry with the largest
+    prob / freq (the first such index on ties; a zero frequency counts as infinitely far
+    behind, a zero probability never receives a count), which is the published allocation
+    of the third-party ``range_coder`` package (unvendored; greedy descent of the KL
+    divergence).  So every non-zero probability gets a non-zero frequency whenever
+    len(prob) <= resolution, the properties other/test_range_coder.py:186-229 pins.  The
+    heap reproduces the sequential argmax exactly: keys are the same float64 quotients and
+    ties resolve to the lower index.  Byte compatibility with the package stays unpinned
+    (no fixture exists), see SURVEY.md §8f."""
+    import heapq
     p = np.asarray(prob, dtype=np.float64).reshape(-1)
     if p.size == 0 or np.any(p < 0) or not np.all(np.isfinite(p)) or p.sum() <= 0:
         raise ValueError("invalid probability vector")
-    nz = p > 0
-    if int(nz.sum()) > resolution:
+    nz = np.flatnonzero(p > 0)
+    if nz.size > resolution:
         raise ValueError("more non-zero probabilities than the resolution")
-    p = p / p.sum()
-    exact = p * resolution
-    freq = np.floor(exact + 1e-9).astype(np.int64)
-    freq[nz & (freq == 0)] = 1
-    diff = int(resolution - freq.sum())
-    if diff > 0:
-        order = sorted(np.flatnonzero(nz), key=lambda i: (-(exact[i] - np.floor(exact[i])), i))
-        for k in range(diff):
-            freq[order[k % len(order)]] += 1
-    elif diff < 0:
-        order = sorted(np.flatnonzero(freq > 1), key=lambda i: ((exact[i] - freq[i]), i))
-        k = 0
-        while diff < 0:
-            i = order[k % len(order)]
-            if freq[i] > 1:
-                freq[i] -= 1
-                diff += 1
-            k += 1
+    freq = np.zeros(p.size, np.int64)
+    # first pass: freq == 0 -> prob / freq = inf for every non-zero entry, lowest index first
+    k = min(int(resolution), nz.size)
+    freq[nz[:k]] = 1
+    heap = [(-(p[i] / 1.0), int(i)) for i in nz[:k]]
+    heapq.heapify(heap)
+    for _ in range(int(resolution) - k):
+        _, i = heapq.heappop(heap)
+        freq[i] += 1
+        heapq.heappush(heap, (-(p[i] / float(freq[i])), i))
     return [0] + [int(v) for v in np.cumsum(freq)]
 
 

@@ -6,7 +6,7 @@ host-side mirror used for weight names/shapes and roofline accounting, and
 ``tests/test_abi.py`` checks the two agree (and agree with the oracle's own,
 independently written tables).
 
-Sources: model_0/model.py:50-246, model_1/model.py (widths 16 at :52/:198),
+Sources: model_0/model.py:50-246, model_1/model.py (widths 16 at :52/:226),
 model_2/model.py:50-193, model_3/model.py:50-300, submit/2/rmbe/model.py:118-189.
 ``res_block`` (basic_block/basic_block.py:74-93) expands into ``<scope>/conv_0`` and
 ``<scope>/conv_1`` (both ReLU); the block input is added after conv_1 (no activation).
