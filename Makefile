@@ -31,7 +31,17 @@ $(LIB): $(OBJS)
 $(BUILD):
 	mkdir -p $(BUILD)
 
+# Host sanitizer build (CPU only): the host C++ that parses user input (range coder,
+# CRC-32C of checkpoint bytes) under AddressSanitizer + UBSan, driven by a fuzz harness.
+ASAN_BIN := $(BUILD)/host_fuzz_asan
+asan: $(ASAN_BIN)
+	$(ASAN_BIN) $(BUILD)
+
+$(ASAN_BIN): tests/native/host_fuzz.cpp $(CSRC)/range_coder.cpp $(CSRC)/host_util.cpp include/tic.h | $(BUILD)
+	g++ -O1 -g -std=c++17 -Wall -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all \
+	    -Iinclude -o $@ tests/native/host_fuzz.cpp $(CSRC)/range_coder.cpp $(CSRC)/host_util.cpp
+
 clean:
 	rm -rf $(BUILD) $(LIB)
 
-.PHONY: all clean
+.PHONY: all clean asan

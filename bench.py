@@ -51,6 +51,10 @@ def parse():
                     help="PMC summary (tools/pmc_summary.py) supplying roofline.traffic; default: the "
                          "committed tools/pmc/traffic_model<N>.json, used only if its source stamp "
                          "matches these kernel sources and its configuration matches this run")
+    ap.add_argument("--tune-cache", default="auto",
+                    help="tuning state (tic_tuning_export) to replay instead of tuning: 'auto' = the "
+                         "committed tools/tune/<config>.json when its source stamp matches (else tune), "
+                         "'none' = always tune, PATH = load if present and matching, else tune and save")
     ap.add_argument("--pmc-plan", default=None,
                     help="PMC mode (tools/pmc_box.sh): tune exactly as the bench does, then run --steps "
                          "steps on ONE lane at the per-lane batch (deterministic dispatch order), write "
@@ -317,10 +321,9 @@ def main():
 
     # per-lane batch: with 2 lanes each kernel launch processes half the batch
     lane_b = -(-B // max(1, min(args.streams, B)))  # largest per-lane part of the batch
+    tuning = "none"
     if not args.no_autotune:
-        codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice, outside the timed region
-        if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
-            codec.autotune_step(d_in, B, rounds=args.tune_step, reps=5)
+        tuning = tune(args, codec, d_in, B, lane_b, M, P)
     if args.pmc_plan:
         return pmc_steady(args, codec, d_in, d_idx, d_rgb, lane_b, M, P)
     for _ in range(args.warmup):
@@ -387,6 +390,7 @@ def main():
         "roofline": roof,
         "roofline_step_frac": round(step_roofline(rows, B, step_ms), 4),
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "hip_graph": bool(args.graph)},
+        "tuning": tuning,
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
                             "raw_bpp": round(summary["bpp"], 4)},
     }
@@ -410,6 +414,35 @@ def main():
         print(json.dumps(out), flush=True)
     comm.close()
     codec.close()
+
+
+def tune_cache_path(args, M, P, B):
+    if args.tune_cache == "none":
+        return None, False
+    if args.tune_cache == "auto":
+        return os.path.join(ROOT, "tools", "tune", f"model{M}_p{P}_b{B}_s{args.streams}.json"), False
+    return args.tune_cache, True
+
+
+def tune(args, codec, d_in, B, lane_b, M, P):
+    """Per-layer autotune + in-situ step tuning (outside the timed region), or the replay of
+    a saved tuning state of the same kernel sources and configuration."""
+    from tf_image_compression_amd._lib import source_digest
+    path, save = tune_cache_path(args, M, P, B)
+    stamp = {"source_sha256": source_digest(), "model": M, "patch": P, "batch": B, "streams": args.streams,
+             "tune_step": args.tune_step}
+    if path and os.path.exists(path):
+        doc = json.load(open(path))
+        if doc.get("_meta") == stamp:
+            codec.tuning_import(doc["tuning"])
+            return os.path.relpath(path, ROOT)
+    codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice
+    if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
+        codec.autotune_step(d_in, B, rounds=args.tune_step, reps=5)
+    if path and save:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        json.dump({"_meta": stamp, "tuning": codec.tuning_export()}, open(path, "w"), indent=1)
+    return "tuned in this run"
 
 
 def pmc_steady(args, codec, d_in, d_idx, d_rgb, lane_b, M, P):

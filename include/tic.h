@@ -139,6 +139,13 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit);
  * form tools/pmc_summary.py prints (e.g. "conv3x3<1,32,32,4,4,1,false,1,false,0,0>");
  * empty when the layer runs inside the previous layer's launch.  cap includes the NUL. */
 int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap);
+/* Tuning state as text (every tuned tiling / variant per layer and batch key, and the
+ * structural fusion flags), so a tuning run can be replayed exactly by another process of
+ * the same build (like cuDNN's find-db): returns the length (excluding the NUL) and writes
+ * it when cap is large enough.  tic_tuning_import validates every entry against the
+ * layer table and the compiled registries (TIC_EINVAL on any mismatch, nothing applied). */
+int tic_tuning_export(const tic_handle* h, char* buf, int cap);
+int tic_tuning_import(tic_handle* h, const char* text);
 
 /* Unit-test entry: one layer on device float32 NHWC tensors.
  * kind/act as tic_layer_info; res (nullable) is added after the activation.

@@ -68,3 +68,14 @@ def test_gloo_world2_sharded_stats(tmp_path):
     psnr = o.dataset_psnr(list(zip(x, y)))
     assert abs(res[0]["summary"]["psnr_db"] - psnr) < 1e-6
     assert res[0]["summary"]["bpp"] == pytest.approx(0.25)
+
+
+def test_unique_id_bytes_keep_zeros():
+    """The 128-byte ncclUniqueId passes through the TCP bootstrap as raw bytes: zero bytes
+    inside it (sockaddr padding) must survive extraction and re-packing (round 1 read it
+    through a c_char field, which cuts at the first NUL)."""
+    raw = bytes([0, 2, 0, 0, 127, 0, 0, 1] + [0] * 40 + list(range(80)))
+    uid = dist.uid_from_bytes(raw)
+    assert dist.uid_to_bytes(uid) == raw
+    with pytest.raises(ValueError):
+        dist.uid_from_bytes(raw[:-1])

@@ -54,6 +54,8 @@ SIGNATURES = [
     ("tic_layer_variant", C.c_int, [vp, C.c_int, C.c_int, i32p, i32p]),
     ("tic_autotune_step", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int]),
     ("tic_layer_kernel", C.c_int, [vp, C.c_int, C.c_int, C.c_char_p, C.c_int]),
+    ("tic_tuning_export", C.c_int, [vp, C.c_char_p, C.c_int]),
+    ("tic_tuning_import", C.c_int, [vp, C.c_char_p]),
     ("tic_conv3x3_device", C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      f32p, f32p, vp, vp]),
     ("tic_get_stream", C.c_int, [vp, C.POINTER(vp)]),

@@ -205,6 +205,16 @@ class Codec:
             out.append(buf.value.decode())
         return out
 
+    def tuning_export(self) -> str:
+        """Tuned tilings / variants / fusion flags as text (tic_tuning_export)."""
+        n = check(lib().tic_tuning_export(self._h, None, 0), "tic_tuning_export")
+        buf = C.create_string_buffer(n + 1)
+        check(lib().tic_tuning_export(self._h, buf, n + 1), "tic_tuning_export")
+        return buf.value.decode()
+
+    def tuning_import(self, text: str) -> None:
+        check(lib().tic_tuning_import(self._h, text.encode()), "tic_tuning_import")
+
     def conv3x3_device(self, kind: int, act: int, d_in: DeviceBuffer, n: int, H: int, W: int, cin: int,
                        cout: int, kernel: np.ndarray, bias: np.ndarray, d_res: DeviceBuffer | None,
                        d_out: DeviceBuffer) -> None:

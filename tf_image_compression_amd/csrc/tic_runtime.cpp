@@ -1624,6 +1624,92 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   return TIC_OK;
 }
 
+int tic_tuning_export(const tic_handle* h, char* buf, int cap) {
+  if (!h || (!buf && cap > 0)) return fail(TIC_EINVAL, "null argument");
+  const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
+                                           tic::conv_registry_t2};
+  std::string t = "tic-tuning 1\n";
+  t += "flag fuse01 " + std::to_string((int)h->fuse01) + "\n";
+  t += "flag fuse_tail " + std::to_string((int)h->fuse_tail) + "\n";
+  t += "flag s1_form " + std::to_string(h->s1_form) + "\n";
+  for (size_t i = 0; i < h->layers.size(); ++i) {
+    const LayerRT& l = h->layers[i];
+    for (const auto& kv : l.tuned) {
+      int cnt = 0;
+      const tic::ConvEntry* base = regs[kv.second->mode](&cnt);
+      t += "conv " + std::to_string(i) + " " + std::to_string(kv.first) + " " + std::to_string(kv.second->mode) +
+           " " + std::to_string(kv.second - base) + "\n";
+    }
+    for (const auto& kv : l.tuned_var)
+      t += "var " + std::to_string(i) + " " + std::to_string(kv.first) + " " + std::to_string(kv.second) + "\n";
+  }
+  if (buf && cap > (int)t.size()) memcpy(buf, t.c_str(), t.size() + 1);
+  return (int)t.size();
+}
+
+int tic_tuning_import(tic_handle* h, const char* text) {
+  if (!h || !text) return fail(TIC_EINVAL, "null argument");
+  const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
+                                           tic::conv_registry_t2};
+  const int L = (int)h->layers.size();
+  std::vector<std::map<int, const tic::ConvEntry*>> tuned(L);
+  std::vector<std::map<int, int>> vars(L);
+  int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form;
+  const char* p = text;
+  int line = 0;
+  while (*p) {
+    const char* e = strchr(p, '\n');
+    std::string ln(p, e ? (size_t)(e - p) : strlen(p));
+    p = e ? e + 1 : p + ln.size();
+    ++line;
+    if (ln.empty()) continue;
+    char kind[16] = "", name[32] = "";
+    int a = 0, b = 0, c = 0, d = 0;
+    if (line == 1) {
+      if (ln != "tic-tuning 1") return fail(TIC_EINVAL, "tuning text: bad header");
+    } else if (sscanf(ln.c_str(), "%15s", kind) != 1) {
+      return fail(TIC_EINVAL, "tuning text line %d: unreadable", line);
+    } else if (!strcmp(kind, "flag")) {
+      if (sscanf(ln.c_str(), "flag %31s %d", name, &a) != 2) return fail(TIC_EINVAL, "tuning line %d", line);
+      if (!strcmp(name, "fuse01")) fuse01 = a != 0;
+      else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
+      else if (!strcmp(name, "s1_form") && (a == 0 || a == 1)) s1_form = a;
+      else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
+    } else if (!strcmp(kind, "conv")) {
+      if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)
+        return fail(TIC_EINVAL, "tuning line %d: bad conv entry", line);
+      int cnt = 0;
+      const tic::ConvEntry* base = regs[c](&cnt);
+      if (d < 0 || d >= cnt) return fail(TIC_EINVAL, "tuning line %d: registry index %d out of range", line, d);
+      const tic::ConvEntry* ce = base + d;
+      const LayerDef& ld = h->layers[a].def;
+      const bool last_enc = !h->rmbe() && a == h->n_enc - 1, first_dec = !h->rmbe() && a == h->n_enc;
+      if (ce->mode != ld.kind || ce->cin != ld.cin || ce->cout != ld.cout || ce->act != ld.act ||
+          ce->res != ld.residual || ce->in != (first_dec ? tic::IN_IDX : tic::IN_F32) ||
+          ce->out != (last_enc ? tic::OUT_QUANT : tic::OUT_F32))
+        return fail(TIC_EINVAL, "tuning line %d: kernel does not match layer %s", line, ld.name.c_str());
+      tuned[a][b] = ce;
+    } else if (!strcmp(kind, "var")) {
+      if (sscanf(ln.c_str(), "var %d %d %d", &a, &b, &c) != 3 || a < 0 || a >= L || c < 0 || c >= 64)
+        return fail(TIC_EINVAL, "tuning line %d: bad var entry", line);
+      vars[a][b] = c;
+    } else {
+      return fail(TIC_EINVAL, "tuning line %d: unknown entry %s", line, kind);
+    }
+  }
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  clear_graphs(h);
+  for (int i = 0; i < L; ++i) {
+    h->layers[i].tuned = tuned[i];
+    h->layers[i].tuned_var = vars[i];
+  }
+  h->fuse01 = fuse01;
+  h->fuse_tail = fuse_tail;
+  h->s1_form = s1_form;
+  return TIC_OK;
+}
+
 int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int n, int H, int W, int cin, int cout,
                        const float* w_host, const float* b_host, const float* d_res, float* d_out) {
   if (!h) return fail(TIC_EINVAL, "null handle");

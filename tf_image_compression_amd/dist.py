@@ -136,7 +136,22 @@ NCCL_UNIQUE_ID_BYTES = 128
 
 
 class _NcclUniqueId(C.Structure):
-    _fields_ = [("internal", C.c_char * NCCL_UNIQUE_ID_BYTES)]
+    # c_ubyte, not c_char: a c_char array field reads back as bytes cut at the first NUL,
+    # and the id (a sockaddr + magic) is full of zero bytes
+    _fields_ = [("internal", C.c_ubyte * NCCL_UNIQUE_ID_BYTES)]
+
+
+def uid_to_bytes(uid: _NcclUniqueId) -> bytes:
+    """All 128 bytes of an ncclUniqueId."""
+    return C.string_at(C.addressof(uid), NCCL_UNIQUE_ID_BYTES)
+
+
+def uid_from_bytes(raw: bytes) -> _NcclUniqueId:
+    if len(raw) != NCCL_UNIQUE_ID_BYTES:
+        raise ValueError(f"ncclUniqueId must be {NCCL_UNIQUE_ID_BYTES} bytes, got {len(raw)}")
+    uid = _NcclUniqueId()
+    C.memmove(C.addressof(uid), raw, NCCL_UNIQUE_ID_BYTES)
+    return uid
 
 
 def _recv_exact(sock, n):
@@ -198,8 +213,8 @@ class RcclComm:
             self._ok(self.nccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = port or int(os.environ.get("TIC_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 17))
-        raw = exchange_unique_id(rank, world, bytes(uid.internal) if rank == 0 else None, addr, port)
-        C.memmove(C.addressof(uid), raw, NCCL_UNIQUE_ID_BYTES)
+        raw = exchange_unique_id(rank, world, uid_to_bytes(uid) if rank == 0 else None, addr, port)
+        uid = uid_from_bytes(raw)
         self.comm = C.c_void_p()
         self._ok(self.nccl.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
         self.stream = codec.stream_ptr()

@@ -22,6 +22,9 @@ dispatch's duration in the SAME pass x 2.4 GHz) — a lower bound, exact at the 
 clock.  No clock is derived from GRBM_GUI_ACTIVE: on dispatches shorter than ~0.3 ms that
 quotient reads high (MI355X_MICROARCH.md, DVFS give-back).
 
+Every pass replays one tuning state (bench.py --tune-cache), and the plans the three
+passes wrote must be identical.
+
 Output: JSON {"_meta": plan meta + source stamp, "units": {unit: {...}}}; bench.py uses it
 for roofline.traffic only when the stamp and configuration match."""
 import csv
@@ -73,15 +76,21 @@ def label(dispatches, plan, steps):
     return out
 
 
-def main(out_dir, plan_path, out_path):
-    plan_doc = json.load(open(plan_path))
-    plan, meta = plan_doc["plan"], dict(plan_doc["_meta"])
-    steps = meta["steps"]
-    passes = {}
+def main(out_dir, out_path):
+    passes, plans = {}, {}
     for kind in ("fetch", "write", "sq"):
         p = os.path.join(out_dir, f"pmc_{kind}", "p_counter_collection.csv")
-        if os.path.exists(p):
-            passes[kind] = label(load(p), plan, steps)
+        pp = os.path.join(out_dir, f"plan_{kind}.json")
+        if os.path.exists(p) and os.path.exists(pp):
+            plans[kind] = json.load(open(pp))
+            passes[kind] = label(load(p), plans[kind]["plan"], plans[kind]["_meta"]["steps"])
+    if not plans:
+        raise SystemExit("no PMC pass found")
+    first = next(iter(plans.values()))
+    plan, meta = first["plan"], dict(first["_meta"])
+    for kind, pd in plans.items():  # every pass must have launched the same kernels
+        if pd["plan"] != plan or pd["_meta"]["source_sha256"] != meta["source_sha256"]:
+            raise SystemExit(f"pass {kind} launched a different plan: the tuning replay did not hold")
     med = lambda v: statistics.median(v) if v else None
     units = {}
     print(f"{'unit':34s} {'kernel':44s} {'us':>7s} {'readMB':>8s} {'writeMB':>8s} {'GB/s':>6s} {'mfma%lb':>7s} {'wait%':>6s}")
