@@ -6,7 +6,7 @@ CSRC     := tf_image_compression_amd/csrc
 BUILD    := build
 LIB      := tf_image_compression_amd/libtic.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -I$(CSRC)
-KERNELS  := conv_s1 conv_s2 conv_t2 conv_rgb image_ops
+KERNELS  := conv_s1 conv_s2 conv_t2 conv_rgb conv_chain image_ops
 OBJS     := $(addprefix $(BUILD)/,$(addsuffix .o,$(KERNELS))) $(BUILD)/tic_runtime.o $(BUILD)/range_coder.o \
             $(BUILD)/host_util.o
 HDRS     := $(wildcard $(CSRC)/*.h) include/tic.h

@@ -1,0 +1,108 @@
+"""wino_chain_kernel (csrc/wino_chain.h): every run of stride-1 64->64 layers in one launch,
+8x8 regions per workgroup with the region borders handed between workgroups.  It
+reproduces the unfused Winograd launches operation for operation, so the bar is bit
+identity with them (pre-activations, symbols, decoder floats and bytes), on every model
+and at patch sizes whose bottleneck is a single partial region (P = 48, 64), 2x2 regions
+(model_0 at 256), 4x4 and 8x8 regions (model_3 at 256: 32x32 and 64x64 stages), and at
+batches whose grid exceeds what the GPU holds at once (the ticket order must keep every
+patch's regions co-resident).  Reference layers: model_0/model.py:98-196,
+model_3/model.py:66-281, submit/2/rmbe/model.py:140-160."""
+import numpy as np
+import pytest
+
+from conftest import structured_patches
+
+pytestmark = pytest.mark.gpu
+
+
+def _codec(model_id, P):
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    return Codec(model_id, synthetic_params(model_id, seed=0), SYNTH_MEAN, SYNTH_STD, patch_size=P)
+
+
+def _run(c, x):
+    idx, pre = c.encode(x, return_preact=True)
+    u8, f = c.decode(idx, return_float=True)
+    return idx, pre, u8, f
+
+
+@pytest.mark.parametrize("model_id,P,n", [(0, 256, 6), (0, 64, 5), (0, 48, 3), (1, 64, 4), (2, 128, 3),
+                                          (3, 128, 3), (3, 256, 3)])
+def test_wino_chain_bit_identical(model_id, P, n):
+    with _codec(model_id, P) as c:
+        x = structured_patches(n, P, seed=600 + model_id + P)
+        c.set_option("s1_form", 1)
+        c.set_option("chain", 0)
+        ref = _run(c, x)
+        assert not any("wino_chain" in k for k in c.layer_kernels(n))
+        c.set_option("chain", 1)
+        kern = c.layer_kernels(n)
+        assert any(k.startswith("wino_chain_kernel") for k in kern), kern
+        got = _run(c, x)
+        for a, b in zip(ref, got):
+            assert np.array_equal(a, b)
+        # lanes split the batch: chain launches on two streams at once
+        c.set_option("streams", 2)
+        assert all(np.array_equal(a, b) for a, b in zip(ref, _run(c, x)))
+        c.set_option("chain", 0)
+
+
+def test_wino_chain_oversubscribed_grid():
+    """model_0 at 256 with 256 patches per launch: 1024 region workgroups on one stream and
+    another 1024 on the second lane, more than are resident at once — the ticket order must
+    still complete every launch, and repeated launches (epochs) stay correct."""
+    with _codec(0, 256) as c:
+        x = structured_patches(8, 256, seed=700)
+        big = np.concatenate([x] * 64)  # 512 patches, 2 lanes x 256
+        c.set_option("chain", 0)
+        ref_idx = c.encode(x)
+        ref_u8 = c.decode(ref_idx)
+        c.set_option("chain", 1)
+        c.set_option("chunk", 512)
+        for _ in range(3):
+            idx = c.encode(big)
+            assert all(np.array_equal(idx[i * 8:(i + 1) * 8], ref_idx) for i in range(64))
+        u8 = c.decode(idx)
+        assert all(np.array_equal(u8[i * 8:(i + 1) * 8], ref_u8) for i in range(64))
+        c.set_option("chain", 0)
+
+
+def test_wino_chain_rmbe_bit_identical():
+    from tf_image_compression_amd.topology import RMBE_ID
+    r = np.random.default_rng(8)
+    win = np.clip(r.normal(120, 50, (5, 128, 128, 3)), 0, 255).astype(np.float32)
+    with _codec(RMBE_ID, 128) as c:
+        c.set_option("chain", 0)
+        a = c.rmbe_windows(win)
+        c.set_option("chain", 1)
+        assert any(k.startswith("wino_chain_kernel") for k in c.layer_kernels(5))
+        b = c.rmbe_windows(win)
+    assert np.array_equal(a, b)
+
+
+def test_wino_chain_device_path_and_tuning_replay():
+    """codec_device with the chain on equals the host path; tic_tuning_export / import
+    carries the chain flag and every tuned choice to a second handle (bit-identical run)."""
+    P, n = 256, 16
+    x = structured_patches(n, P, seed=710)
+    with _codec(0, P) as c:
+        c.set_option("chain", 1)
+        idx, u8 = c.encode(x), None
+        u8 = c.decode(idx)
+        d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(idx.nbytes), c.alloc(x.nbytes)
+        d_in.upload(x)
+        c.autotune(d_in, n // 2, reps=1)
+        c.codec_device(d_in, n, d_idx, d_rgb)
+        c.synchronize()
+        assert np.array_equal(d_idx.download(idx.shape, np.uint8), idx)
+        assert np.array_equal(d_rgb.download(x.shape, np.uint8), u8)
+        text = c.tuning_export()
+        assert "flag chain 1" in text
+        with _codec(0, P) as c2:
+            c2.tuning_import(text)
+            assert c2.tuning_export() == text
+            assert c2.layer_kernels(n // 2) == c.layer_kernels(n // 2)
+            assert np.array_equal(c2.encode(x), idx)
+            with pytest.raises(ValueError):
+                c2.tuning_import("tic-tuning 1\nconv 0 8 2 0\n")  # a T2 kernel for the first layer

@@ -111,6 +111,11 @@ bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int vari
 int dec10_variants();
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant);
 
+// A chain of stride-1 64->64 layers in one launch (wino_chain.h, conv_chain.hip): args in
+// wino_chain.h; false if the mode combination is not compiled.
+struct ChainArgs;
+bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s);
+
 // Whole-image glue and the symbol histogram (image_ops.hip).
 void launch_tile_reflect(const uint8_t* img, int H, int W, int P, int hn, int wn, uint8_t* out, int num_cus,
                          hipStream_t s);

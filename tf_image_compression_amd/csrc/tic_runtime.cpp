@@ -21,6 +21,7 @@
 
 #include "../../include/tic.h"
 #include "tic_kernels.h"
+#include "wino_chain.h"
 
 namespace {
 
@@ -336,6 +337,13 @@ struct Lane {
   hipStream_t stream = nullptr;
   float* ws[3] = {nullptr, nullptr, nullptr};
   int ws_batch = 0;
+  // wino_chain_kernel hand-off state (border exchange, per-(layer, region) flags, ticket /
+  // epoch / error words), shared by every chain launch of this lane (stream-ordered)
+  float* xbuf = nullptr;
+  size_t xbuf_floats = 0;
+  unsigned* cflags = nullptr;
+  size_t cflags_n = 0;
+  unsigned* ctl = nullptr;
 };
 
 struct tic_handle {
@@ -372,6 +380,7 @@ struct tic_handle {
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
+  bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   struct GraphKey {
     const void *in, *idx, *rgb;
     int n, nlanes;
@@ -420,6 +429,50 @@ int ensure_ws(tic_handle* h, Lane& ln, int n) {
   ln.ws_batch = 0;
   for (auto& b : ln.ws) HIP_TRY(hipMalloc((void**)&b, h->act_elems * (size_t)n * sizeof(float)));
   ln.ws_batch = n;
+  return TIC_OK;
+}
+
+// Grow a lane's chain hand-off buffers for a chain of nl layers over n patches of R
+// regions.  Fresh flags are zero, below every launch's epoch + 1, so nothing else is reset.
+int ensure_chain(tic_handle* h, Lane& ln, int nl, int n, int R) {
+  const size_t nR = (size_t)n * R;
+  const size_t xf = (size_t)(nl - 1) * nR * 4 * 8 * 64, nf = (size_t)(nl - 1) * nR;
+  if (!ln.ctl) {
+    HIP_TRY(hipMalloc((void**)&ln.ctl, 4 * sizeof(unsigned)));
+    HIP_TRY(hipMemsetAsync(ln.ctl, 0, 4 * sizeof(unsigned), ln.stream));
+  }
+  if (ln.xbuf_floats < xf) {
+    clear_graphs(h);
+    if (ln.xbuf) (void)hipFree(ln.xbuf);
+    ln.xbuf = nullptr;
+    ln.xbuf_floats = 0;
+    HIP_TRY(hipMalloc((void**)&ln.xbuf, std::max<size_t>(xf, 64) * sizeof(float)));
+    ln.xbuf_floats = xf;
+  }
+  if (ln.cflags_n < nf) {
+    clear_graphs(h);
+    if (ln.cflags) (void)hipFree(ln.cflags);
+    ln.cflags = nullptr;
+    ln.cflags_n = 0;
+    HIP_TRY(hipMalloc((void**)&ln.cflags, std::max<size_t>(nf, 16) * sizeof(unsigned)));
+    HIP_TRY(hipMemsetAsync(ln.cflags, 0, std::max<size_t>(nf, 16) * sizeof(unsigned), ln.stream));
+    ln.cflags_n = nf;
+  }
+  return TIC_OK;
+}
+
+// A chain hand-off that timed out (wino_chain_kernel's bounded poll) leaves an error word;
+// report it (and clear it) at the next synchronisation point.
+int check_chain_error(tic_handle* h) {
+  for (Lane& ln : h->lanes) {
+    if (!ln.ctl) continue;
+    unsigned w[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpy(w, ln.ctl, sizeof w, hipMemcpyDeviceToHost));
+    if (w[3]) {
+      HIP_TRY(hipMemset(ln.ctl + 3, 0, sizeof(unsigned)));
+      return fail(TIC_EHIP, "wino_chain_kernel: a region hand-off timed out (results of that launch are invalid)");
+    }
+  }
   return TIC_OK;
 }
 
@@ -516,6 +569,37 @@ static bool fuses_tail(const tic_handle* h) {
   const LayerDef& d = h->layers[L - 2].def;
   const bool ok = (d.cin == 32 && d.cout == 32) || (d.cin == 32 && d.cout == 16) || (d.cin == 64 && d.cout == 32);
   return ok && d.kind == K_T2 && d.act == 1 && !d.residual && !(!h->rmbe() && L - 2 == h->n_enc);
+}
+
+// wino_chain_kernel: layers [li, chain_end) run in one launch when the handle's "chain"
+// option is on, the stride-1 form is Winograd (the chain reproduces it bit for bit) and
+// li starts a run of >= 2 stride-1 64->64 layers inside one network half (the encoder's
+// last layer may end a run with the quantiser, the decoder's first may start one with the
+// dequantiser).  Returns li when no chain starts there.
+static int chain_end(const tic_handle* h, int li) {
+  const int L = (int)h->layers.size();
+  if (!h->chain || h->s1_form != 1 || li == 0 || li >= L - 1) return li;
+  auto s1_64 = [&](int i) {
+    const LayerDef& d = h->layers[i].def;
+    return d.kind == K_S1 && d.cin == 64 && d.cout == 64 && i > 0 && i < L - 1;
+  };
+  if (!s1_64(li)) return li;
+  const bool first_dec = !h->rmbe() && li == h->n_enc;
+  if (!first_dec && s1_64(li - 1) && (h->rmbe() || li - 1 != h->n_enc - 1)) return li;  // not a run start
+  int j = li + 1;
+  while (j < L - 1 && j - li < tic::CH_MAX_LAYERS && s1_64(j) && (h->rmbe() || j != h->n_enc)) ++j;
+  return j - li >= 2 ? j : li;
+}
+// layer i runs inside some wino_chain_kernel launch
+static bool in_chain(const tic_handle* h, int i) {
+  for (int s = 1; s <= i; ++s)
+    if (chain_end(h, s) > i) return true;  // a chain starting at s covers s..chain_end-1
+  return false;
+}
+static bool any_chain(const tic_handle* h) {
+  for (int i = 0; i < (int)h->layers.size(); ++i)
+    if (chain_end(h, i) > i) return true;
+  return false;
 }
 
 // Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
@@ -622,6 +706,47 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         HIP_TRY(hipEventRecord(prof.ev[2 * li + 3], st));
       }
       break;
+    }
+    const int ce = chain_end(h, li);
+    if (ce > li && ce <= l1) {
+      const int nl = ce - li;
+      const bool last_enc_c = !h->rmbe() && ce - 1 == h->n_enc - 1;
+      const int R = ((lay.h_in + 7) / 8) * ((lay.h_in + 7) / 8);
+      int rc = ensure_chain(h, ln, nl, n, R);
+      if (rc) return rc;
+      tic::ChainArgs a{};
+      for (int k = 0; k < nl; ++k) {
+        const LayerRT& lk = h->layers[li + k];
+        a.layer[k] = {lk.d_ww, lk.d_b, lk.def.act, lk.def.residual};
+      }
+      a.nl = nl;
+      a.in = first_dec ? in : (const void*)src;
+      a.lut = h->d_lut;
+      a.out = last_enc_c ? d_pre : ws[dst];
+      a.qout = last_enc_c ? d_idx : nullptr;
+      a.qscale = (float)(h->Q - 1);
+      a.H = a.W = lay.h_in;
+      a.rh = a.rw = (lay.h_in + 7) / 8;
+      a.n = n;
+      a.xbuf = ln.xbuf;
+      a.flags = ln.cflags;
+      a.ctl = ln.ctl;
+      if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
+                                  st))
+        return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);
+      rc = check_launch();
+      if (rc) return rc;
+      if (prof.ev) {
+        HIP_TRY(hipEventRecord(prof.ev[2 * li + 1], st));
+        for (int k = li + 1; k < ce; ++k) {  // the other layers ran inside this launch
+          HIP_TRY(hipEventRecord(prof.ev[2 * k], st));
+          HIP_TRY(hipEventRecord(prof.ev[2 * k + 1], st));
+        }
+      }
+      block_in = -1;
+      cur = dst;
+      li = ce - 1;
+      continue;
     }
     if (first) {
       tic::RgbInArgs a{};
@@ -933,6 +1058,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE01")) h->fuse01 = atoi(f) != 0;
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   else h->fuse_tail = kFuseTailDefault;
+  if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   for (int i = 1; i < 4 && e == hipSuccess; ++i) {
     e = hipStreamCreateWithFlags(&h->lanes[i].stream, hipStreamNonBlocking);
@@ -960,9 +1086,13 @@ void tic_destroy(tic_handle* h) {
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
-  for (auto& ln : h->lanes)
+  for (auto& ln : h->lanes) {
     for (auto& b : ln.ws)
       if (b) (void)hipFree(b);
+    if (ln.xbuf) (void)hipFree(ln.xbuf);
+    if (ln.cflags) (void)hipFree(ln.cflags);
+    if (ln.ctl) (void)hipFree(ln.ctl);
+  }
   for (int i = 1; i < 4; ++i) {
     if (h->lanes[i].stream) {
       (void)hipStreamSynchronize(h->lanes[i].stream);
@@ -1129,7 +1259,7 @@ int tic_memcpy_d2h(tic_handle* h, void* dst, const void* src, size_t bytes) {
 int tic_synchronize(tic_handle* h) {
   if (!h) return fail(TIC_EINVAL, "null handle");
   HIP_TRY(hipStreamSynchronize(h->stream));
-  return TIC_OK;
+  return check_chain_error(h);
 }
 
 int tic_encode_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_idx, float* d_preact) {
@@ -1220,6 +1350,12 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->fuse_tail = value != 0;
     return TIC_OK;
   }
+  if (k == "chain") {  // stride-1 runs in one wino_chain_kernel launch (Winograd form only)
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->chain = value != 0;
+    return TIC_OK;
+  }
   if (k == "s1_form") {  // 0 direct, 1 Winograd, -1 the default (TIC_S1_FORM or built-in)
     if (value < -1 || value > 1) return fail(TIC_EINVAL, "s1_form must be -1, 0 or 1");
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1256,7 +1392,7 @@ int tic_encode(tic_handle* h, const uint8_t* patches, int n, uint8_t* idx_out, f
   HIP_TRY(hipMemcpyAsync(idx_out, h->st_out, ce, hipMemcpyDeviceToHost, h->stream));
   if (preact_out) HIP_TRY(hipMemcpyAsync(preact_out, h->st_out2, ce * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  return TIC_OK;
+  return check_chain_error(h);
 }
 
 int tic_decode(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb_out, float* f32_out) {
@@ -1277,7 +1413,7 @@ int tic_decode(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb_out, float
   if (rgb_out) HIP_TRY(hipMemcpyAsync(rgb_out, h->st_out, px, hipMemcpyDeviceToHost, h->stream));
   if (f32_out) HIP_TRY(hipMemcpyAsync(f32_out, h->st_out2, px * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  return TIC_OK;
+  return check_chain_error(h);
 }
 
 int tic_rmbe(tic_handle* h, const float* windows, int n, float* out) {
@@ -1294,7 +1430,7 @@ int tic_rmbe(tic_handle* h, const float* windows, int n, float* out) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out, h->st_out2, b, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  return TIC_OK;
+  return check_chain_error(h);
 }
 
 int tic_num_layers(const tic_handle* h) {
@@ -1404,6 +1540,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       const LayerRT& l = h->layers[i];
       const bool rgb = i == 0 || i + 1 == h->layers.size();
       if (i + 2 >= h->layers.size() && fuses_tail(h)) continue;  // runs inside dec10_kernel
+      if (in_chain(h, (int)i)) continue;                          // runs inside wino_chain_kernel
       if (rgb ? !l.tuned_var.count(m) : !l.tuned.count(tkey(h, l, m))) have = false;
     }
     if (!have) {
@@ -1456,7 +1593,8 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     const char* env;
     const char* name;
   };
-  const Flag flags[2] = {{&h->fuse_tail, fuses_tail, "TIC_FUSE_TAIL", "fuse_tail"},
+  const Flag flags[3] = {{&h->chain, any_chain, "TIC_CHAIN", "chain"},
+                         {&h->fuse_tail, fuses_tail, "TIC_FUSE_TAIL", "fuse_tail"},
                          {&h->fuse01, fuses01, "TIC_FUSE01", "fuse01"}};
   for (const Flag& f : flags) {
     if (rc || getenv(f.env)) continue;
@@ -1482,6 +1620,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       const bool first = i == 0, last = i == L - 1;
       if ((first || i == 1) && fuses01(h)) continue;
       if (i >= L - 2 && fuses_tail(h)) continue;
+      if (in_chain(h, i)) continue;
       if (first || last) {
         const RgbOutForm fm = first ? RgbOutForm{0, tic::rgb_in_variants()} : rgb_out_form();
         const int keep = first ? l.tuned_var[sizes[0]] : rgb_out_variant(l.tuned_var, sizes[0]);
@@ -1573,7 +1712,16 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   const int L = (int)h->layers.size();
   const char* tf[2] = {"false", "true"};
   char buf[160] = "";
-  if (fuses_tail(h) && i >= L - 2) {
+  int cs = -1;  // start of the chain containing layer i
+  for (int s0 = 1; s0 <= i; ++s0)
+    if (chain_end(h, s0) > i && chain_end(h, s0) > s0) cs = s0;
+  if (cs >= 0) {
+    if (cs == i) {
+      const int ce = chain_end(h, cs);
+      const bool first_dec = !h->rmbe() && cs == h->n_enc, last_enc = !h->rmbe() && ce - 1 == h->n_enc - 1;
+      snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0);
+    }
+  } else if (fuses_tail(h) && i >= L - 2) {
     if (i == L - 2) {
       auto iv = l.tuned_var.find(n);
       int v = iv != l.tuned_var.end() ? iv->second : 0;
@@ -1632,6 +1780,7 @@ int tic_tuning_export(const tic_handle* h, char* buf, int cap) {
   t += "flag fuse01 " + std::to_string((int)h->fuse01) + "\n";
   t += "flag fuse_tail " + std::to_string((int)h->fuse_tail) + "\n";
   t += "flag s1_form " + std::to_string(h->s1_form) + "\n";
+  t += "flag chain " + std::to_string((int)h->chain) + "\n";
   for (size_t i = 0; i < h->layers.size(); ++i) {
     const LayerRT& l = h->layers[i];
     for (const auto& kv : l.tuned) {
@@ -1654,7 +1803,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   const int L = (int)h->layers.size();
   std::vector<std::map<int, const tic::ConvEntry*>> tuned(L);
   std::vector<std::map<int, int>> vars(L);
-  int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form;
+  int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form, chain = h->chain;
   const char* p = text;
   int line = 0;
   while (*p) {
@@ -1674,6 +1823,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       if (!strcmp(name, "fuse01")) fuse01 = a != 0;
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
       else if (!strcmp(name, "s1_form") && (a == 0 || a == 1)) s1_form = a;
+      else if (!strcmp(name, "chain")) chain = a != 0;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
     } else if (!strcmp(kind, "conv")) {
       if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)
@@ -1707,6 +1857,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   h->fuse01 = fuse01;
   h->fuse_tail = fuse_tail;
   h->s1_form = s1_form;
+  h->chain = chain;
   return TIC_OK;
 }
 

@@ -1,0 +1,402 @@
+// wino_chain.h — a chain of stride-1 3x3 64->64 convolutions in ONE launch: the residual
+// stages of the codecs (basic_block.res_block, basic_block/basic_block.py:74-93) with the
+// plain stride-1 layer on either side of them — model_0/1 encode_res_1..encode_4 with the
+// quantiser (model_0/model.py:98-144) and decode_4 (dequantiser LUT) .. decode_res_2
+// (:148-196); model_3's residual stages at H/4 and H/8 (model_3/model.py:66-150,191-281);
+// the rmbe net's conv_3/conv_4 (submit/2/rmbe/model.py:140-160).
+//
+// Form: Winograd F(2x2,3x3) exactly as conv3x3_wino_kernel computes it — same U packing,
+// same B^T d B in registers, same MFMA K order (16-channel chunk, t, lane group), same
+// A^T M A and the same epilogue — so every layer's output is bit-identical to the unfused
+// launch of that layer (tests/test_gpu_parity.py::test_wino_chain_bit_identical).
+//
+// Decomposition: one 256-thread workgroup owns an 8x8 output REGION of one patch for every
+// layer of the chain (16 Winograd tiles = one 16-tile MFMA block; wave xi owns the
+// transform points (xi, 0..3)); the region's 10x10 input tile (1-pixel halo) stays in LDS
+// from layer to layer.  Between layers a region needs its neighbours' border pixels: each
+// workgroup publishes its 32 border pixels (rows 0 and 7, columns 0 and 7; 8 KB) with
+// write-through (sc1) 8-byte stores, drains them, and raises a per-(layer, region) flag;
+// the neighbours poll the flags with sc1 loads and read the halo with sc1 loads
+// (MI355X_MICROARCH.md, valid hand-off form, row 1).  No redundant halo recomputation,
+// ~1 hand-off per layer instead of a kernel boundary + full activation round trip.
+//
+// Progress: the regions of a patch wait for each other, so they must be co-resident.
+// Work is handed out by a ticket (one atomic per workgroup at start): a workgroup that runs
+// holds ticket t only if tickets 0..t-1 were taken by workgroups that are running or done,
+// so the regions of one patch (consecutive tickets) never wait on a region that cannot be
+// scheduled — at most the last patch is incomplete, and the workgroups ahead of it finish
+// without waiting on it.  Every poll is bounded as well (error flag, never a hang).
+// The last workgroup to finish resets the ticket and advances the launch epoch that the
+// flags are compared against, so no buffer needs clearing between launches.
+#pragma once
+#include "conv3x3_wino.h"
+
+namespace tic {
+
+constexpr int CH_MAX_LAYERS = 8;
+
+struct ChainLayer {
+  const float* wu;    // Winograd U [16 p][4 kc][4 g][64][4 t] (pack_wino)
+  const float* bias;  // [64]
+  int act;            // ACT_ID / ACT_RELU
+  int res;            // + the res_block input after the activation (res_block conv_1)
+};
+
+struct ChainArgs {
+  ChainLayer layer[CH_MAX_LAYERS];
+  int nl;               // layers in the chain (2..CH_MAX_LAYERS)
+  const void* in;       // first layer's input: f32 [n,H,W,64] or u8 symbols (IN_IDX)
+  const float* lut;     // IN_IDX: dequantiser table
+  float* out;           // last layer: f32 [n,H,W,64] (OUT_F32) / optional pre-activation (OUT_QUANT)
+  uint8_t* qout;        // OUT_QUANT: u8 symbols [n,H,W,64]
+  float qscale;         // Q - 1
+  int H, W;             // spatial size of every layer (stride 1)
+  int rh, rw;           // 8x8 regions per patch: ceil(H/8) x ceil(W/8)
+  int n;                // patches
+  float* xbuf;          // border exchange [nl-1][n*R][4 sides][8 px][64] f32
+  unsigned* flags;      // [nl-1][n*R] epoch flags
+  unsigned* ctl;        // [0] ticket, [1] done count, [2] epoch, [3] error (poll timeout)
+};
+
+namespace chain {
+constexpr int C = 64, PS = 72, KC = 4;  // channels, LDS pixel stride (floats), 16-ch chunks
+constexpr int HP = 5, RP = 10, LR = 10; // parity half-row, row pitch (pixels), rows: 10x10 tile
+constexpr int NT = 16, TTX = 4;         // 2x2 tiles per region, tiles per tile row
+constexpr int XS = C + 8;               // T-exchange pitch
+constexpr int TILE = LR * RP * PS;      // 7200 floats
+constexpr int XCH = 8 * NT * XS;        // 9216 floats
+constexpr int TB = TILE > XCH ? TILE : XCH;
+constexpr unsigned kSpinLimit = 1u << 22;  // ~0.5 s of polling before the error flag
+
+// LDS float offset of staged pixel (row, col) of a 10x10 tile (columns split by parity)
+__device__ __forceinline__ int tpix(int row, int col) { return (row * RP + (col & 1) * HP + (col >> 1)) * PS; }
+
+__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  const unsigned long long lo = (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
+  const unsigned long long hi = (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32);
+  __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return f32x4{__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)), __uint_as_float((unsigned)hi),
+               __uint_as_float((unsigned)(hi >> 32))};
+}
+}  // namespace chain
+
+// IN: IN_F32 / IN_IDX for the first layer; OUT: OUT_F32 / OUT_QUANT for the last one.
+template <int IN, int OUT>
+__global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
+  using namespace chain;
+  __shared__ __attribute__((aligned(16))) float smem[2 * TB];
+  __shared__ unsigned sh[2];
+  const int tid = threadIdx.x;
+  const int xi = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
+  const int H = a.H, W = a.W, R = a.rh * a.rw, nR = a.n * R;
+
+  if (tid == 0) {
+    sh[0] = __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[1] = __hip_atomic_load(&a.ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int ticket = (int)sh[0];
+  const unsigned epoch = sh[1] + 1u;  // this launch's flag value
+  const int nimg = ticket / R, reg = ticket % R;
+  const int ry = reg / a.rw, rx = reg % a.rw;
+  const int oy0 = ry * 8, ox0 = rx * 8;
+
+  // ---- weights of layer l, step s = 4 kc + nu, straight from L2, prefetched PF ahead ----
+  constexpr int NSTEP = 4 * KC, PF = 3, NBW = 4;
+  f32x4 av[PF + 1][NBW];
+  auto wglob = [&](int l, int s, int nb) -> f32x4 {
+    const int kc = s >> 2, nu = s & 3;
+    const float* wl = a.layer[l].wu + (size_t)xi * 64 * KC * C + (size_t)(lg * C + li) * 4;
+    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * C + nb * 64);
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(0, p, nb);
+
+  // ---- stage the first layer's input tile (zero outside the image = SAME padding) ----
+  // The first layer's tile is the res_block input when the chain starts a block, so it
+  // goes to tile 0 (A) then, else to tile 1 (B): the block input always lives in A.
+  const bool first_block = a.nl > 1 && a.layer[1].res;
+  float* src = first_block ? smem : smem + TB;
+  {
+    constexpr int NSTAGE = LR * 10 * (C / 4);  // 1600 16-byte chunks
+    constexpr int NIT = (NSTAGE + 255) / 256;
+    f32x4 tmp[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = i * 256 + tid;
+      tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (e < NSTAGE) {
+        const int c4 = e % 16, pe = e / 16, col = pe % 10, row = pe / 10;
+        const int iy = oy0 - 1 + row, ix = ox0 - 1 + col;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+          const size_t off = ((size_t)(nimg * H + iy) * W + ix) * C + c4 * 4;
+          if constexpr (IN == IN_F32) {
+            tmp[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
+          } else {
+            const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
+            tmp[i].x = a.lut[q & 0xff];
+            tmp[i].y = a.lut[(q >> 8) & 0xff];
+            tmp[i].z = a.lut[(q >> 16) & 0xff];
+            tmp[i].w = a.lut[q >> 24];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int e = i * 256 + tid;
+      if (e < NSTAGE) {
+        const int c4 = e % 16, pe = e / 16, col = pe % 10, row = pe / 10;
+        *reinterpret_cast<f32x4*>(&src[tpix(row, col) + c4 * 4]) = tmp[i];
+      }
+    }
+  }
+  __syncthreads();
+
+  // B^T row xi from input rows iA, iB of each tile (conv3x3_wino_kernel's exact signs)
+  const int iA = xi == 0 ? 0 : 1, iB = xi == 3 ? 3 : 2;
+  const float sA = xi == 2 ? -1.f : 1.f, sB = (xi == 0 || xi == 3) ? -1.f : 1.f;
+  const int ty_l = li / TTX, tx_l = li % TTX;
+  const int offA = ((2 * ty_l + iA) * RP + tx_l) * PS + lg * 4;
+  const int offB = ((2 * ty_l + iB) * RP + tx_l) * PS + lg * 4;
+  // epilogue ownership: one (tile, channel quad) per thread
+  const int et = tid >> 4, eq = tid & 15;
+  const int ety = et / TTX, etx = et % TTX;
+  bool failed = false;
+
+  for (int l = 0; l < a.nl; ++l) {
+    const bool last = l == a.nl - 1;
+    const bool res = a.layer[l].res != 0;
+    const bool starts_block = !last && a.layer[l + 1].res != 0;
+    float* const dst = src == smem ? smem + TB : smem;  // the other tile
+    float* const xch = starts_block ? dst : src;        // T exchange: never the block input
+    float* const rsd = dst;                              // res layers: the block input tile
+
+    // ---- K loop: conv3x3_wino_kernel's order ----
+    f32x4 d[2][4];
+    auto load_d = [&](int kc) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cj = ((j & 1) * HP + (j >> 1)) * PS + kc * 16;
+        d[0][j] = *reinterpret_cast<const f32x4*>(&src[offA + cj]);
+        d[1][j] = *reinterpret_cast<const f32x4*>(&src[offB + cj]);
+      }
+    };
+    f32x4 V[4];
+    auto transform = [&]() {
+      f32x4 r[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = sA * d[0][j] + sB * d[1][j];
+      V[0] = r[0] - r[2];
+      V[1] = r[1] + r[2];
+      V[2] = r[2] - r[1];
+      V[3] = r[1] - r[3];
+    };
+    f32x4 acc[4][NBW];
+#pragma unroll
+    for (int nu = 0; nu < 4; ++nu)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    load_d(0);
+    transform();
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      if (kc + 1 < KC) load_d(kc + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nu = 0; nu < 4; ++nu) {
+        const int s = kc * 4 + nu;
+        if (s + PF < NSTEP) {
+#pragma unroll
+          for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(l, s + PF, nb);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = mfma4(av[s % (PF + 1)][nb][t], V[nu][t], acc[nu][nb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (kc + 1 < KC) transform();
+    }
+    // the next layer's first weight steps fly during this layer's epilogue and hand-off
+    if (!last) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(l + 1, p, nb);
+    }
+
+    // ---- T = M A over nu, exchanged through LDS ----
+    __syncthreads();  // every wave is done reading src (xch may alias it)
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) {
+      const f32x4 m0 = acc[0][nb], m1 = acc[1][nb], m2 = acc[2][nb], m3 = acc[3][nb];
+      float* x = &xch[(xi * 2 * NT + li) * XS + nb * 16 + lg * 4];
+      *reinterpret_cast<f32x4*>(x) = (m0 + m1) + m2;
+      *reinterpret_cast<f32x4*>(x + NT * XS) = (m1 - m2) - m3;
+    }
+    __syncthreads();
+
+    // ---- Y = A^T T for (tile et, quad eq), + bias, act, + residual ----
+    f32x4 T[4][2];
+#pragma unroll
+    for (int x2 = 0; x2 < 4; ++x2)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) T[x2][b] = *reinterpret_cast<const f32x4*>(&xch[((x2 * 2 + b) * NT + et) * XS + 4 * eq]);
+    const int co = 4 * eq;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(a.layer[l].bias + co);
+    const bool relu = a.layer[l].act == ACT_RELU;
+    f32x4 y[2][2];
+#pragma unroll
+    for (int ay = 0; ay < 2; ++ay)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x4 v = ay == 0 ? (T[0][b] + T[1][b]) + T[2][b] : (T[1][b] - T[2][b]) - T[3][b];
+        v.x = __fadd_rn(v.x, bb.x);
+        v.y = __fadd_rn(v.y, bb.y);
+        v.z = __fadd_rn(v.z, bb.z);
+        v.w = __fadd_rn(v.w, bb.w);
+        if (relu) {
+          v.x = fmaxf(v.x, 0.f);
+          v.y = fmaxf(v.y, 0.f);
+          v.z = fmaxf(v.z, 0.f);
+          v.w = fmaxf(v.w, 0.f);
+        }
+        if (res) {
+          const f32x4 rr = *reinterpret_cast<const f32x4*>(&rsd[tpix(2 * ety + ay + 1, 2 * etx + b + 1) + co]);
+          v.x = __fadd_rn(v.x, rr.x);
+          v.y = __fadd_rn(v.y, rr.y);
+          v.z = __fadd_rn(v.z, rr.z);
+          v.w = __fadd_rn(v.w, rr.w);
+        }
+        y[ay][b] = v;
+      }
+
+    if (last) {  // ---- the chain's output: global f32 or the quantiser ----
+#pragma unroll
+      for (int ay = 0; ay < 2; ++ay)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int oy = oy0 + 2 * ety + ay, ox = ox0 + 2 * etx + b;
+          if (oy >= H || ox >= W) continue;
+          const size_t o = ((size_t)(nimg * H + oy) * W + ox) * C + co;
+          const f32x4 v = y[ay][b];
+          if constexpr (OUT == OUT_F32) {
+            *reinterpret_cast<f32x4*>(a.out + o) = v;
+          } else {
+            if (a.out) *reinterpret_cast<f32x4*>(a.out + o) = v;
+            const uint32_t q = quant1(v.x, a.qscale) | (quant1(v.y, a.qscale) << 8) |
+                               (quant1(v.z, a.qscale) << 16) | (quant1(v.w, a.qscale) << 24);
+            *reinterpret_cast<uint32_t*>(a.qout + o) = q;
+          }
+        }
+      break;
+    }
+
+    // ---- into the next layer's tile (interior), zero outside the image ----
+    if (xch == dst) __syncthreads();  // every thread has read its T from dst's space
+#pragma unroll
+    for (int ay = 0; ay < 2; ++ay)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ly = 2 * ety + ay, lx = 2 * etx + b;
+        const bool in_img = oy0 + ly < H && ox0 + lx < W;
+        *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[ay][b] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    __syncthreads();
+
+    // ---- hand-off: publish this region's border, then read the neighbours' ----
+    if (R > 1) {
+      const size_t g = (size_t)nimg * R + reg;
+      float* const xb = a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {  // 4 sides x 8 pixels x 16 quads = 512 chunks
+        const int e = k * 256 + tid;
+        const int side = e >> 7, px = (e >> 4) & 7, q = e & 15;
+        const int ly = side == 0 ? 0 : (side == 1 ? 7 : px), lx = side == 2 ? 0 : (side == 3 ? 7 : px);
+        st_sc1(xb + (side * 8 + px) * C + 4 * q, *reinterpret_cast<const f32x4*>(&dst[tpix(ly + 1, lx + 1) + 4 * q]));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(&a.flags[(size_t)l * nR + g], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // wait for the (up to 8) neighbours' flags of this layer
+      if (tid < 9 && tid != 4) {
+        const int nry = ry + tid / 3 - 1, nrx = rx + tid % 3 - 1;
+        if (nry >= 0 && nry < a.rh && nrx >= 0 && nrx < a.rw) {
+          const unsigned* f = &a.flags[(size_t)l * nR + (size_t)nimg * R + nry * a.rw + nrx];
+          unsigned it = 0;
+          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            if (++it > kSpinLimit) {
+              failed = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+      }
+      __syncthreads();
+      // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16 quads
+      for (int e = tid; e < 36 * 16; e += 256) {
+        const int hp = e >> 4, q = e & 15;
+        int hy, hx;
+        if (hp < 10) hy = -1, hx = hp - 1;
+        else if (hp < 20) hy = 8, hx = hp - 11;
+        else if (hp < 28) hy = hp - 20, hx = -1;
+        else hy = hp - 28, hx = 8;
+        const int gy = oy0 + hy, gx = ox0 + hx;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+          const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
+          const int ny = hy & 7, nx = hx & 7;  // pixel inside the neighbour region
+          int side, idx;
+          if (hy < 0) side = 1, idx = nx;
+          else if (hy > 7) side = 0, idx = nx;
+          else if (hx < 0) side = 3, idx = ny;
+          else side = 2, idx = ny;
+          const size_t gn = (size_t)nimg * R + nry * a.rw + nrx;
+          v = ld_sc1(a.xbuf + ((size_t)l * nR + gn) * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q);
+        }
+        *reinterpret_cast<f32x4*>(&dst[tpix(hy + 1, hx + 1) + 4 * q]) = v;
+      }
+      __syncthreads();
+    } else {
+      // a single region per patch: the halo is all outside the image
+      for (int e = tid; e < 36 * 16; e += 256) {
+        const int hp = e >> 4, q = e & 15;
+        int hy, hx;
+        if (hp < 10) hy = -1, hx = hp - 1;
+        else if (hp < 20) hy = 8, hx = hp - 11;
+        else if (hp < 28) hy = hp - 20, hx = -1;
+        else hy = hp - 28, hx = 8;
+        *reinterpret_cast<f32x4*>(&dst[tpix(hy + 1, hx + 1) + 4 * q]) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+    }
+    src = dst;
+  }
+
+  // ---- the last workgroup to finish resets the ticket and advances the epoch ----
+  if (failed) __hip_atomic_store(&a.ctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned done = __hip_atomic_fetch_add(&a.ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(&a.ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ctl[2], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace tic
