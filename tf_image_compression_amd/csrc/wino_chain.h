@@ -66,7 +66,7 @@ constexpr int XS = C + 8;               // T-exchange pitch
 constexpr int TILE = LR * RP * PS;      // 7200 floats
 constexpr int XCH = 8 * NT * XS;        // 9216 floats
 constexpr int TB = TILE > XCH ? TILE : XCH;
-constexpr unsigned kSpinLimit = 1u << 22;  // ~0.5 s of polling before the error flag
+constexpr unsigned kSpinLimit = 1u << 19;  // ~0.5 s of polling before the error flag
 
 // LDS float offset of staged pixel (row, col) of a 10x10 tile (columns split by parity)
 __device__ __forceinline__ int tpix(int row, int col) { return (row * RP + (col & 1) * HP + (col >> 1)) * PS; }
