@@ -204,6 +204,9 @@ __global__ void __launch_bounds__(256) conv3x3_wino_kernel(const ConvArgs a) {
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
       }
+      // keep each weight load PF steps ahead of its use (the scheduler otherwise sinks the
+      // loads next to their consumers inside the chunk and the prefetch collapses)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -211,6 +214,7 @@ __global__ void __launch_bounds__(256) conv3x3_wino_kernel(const ConvArgs a) {
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb)
             acc[nu][nn][nb] = mfma4(av[s % (PF + 1)][nb][t], V[nn][nu][t], acc[nu][nn][nb]);
+      __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (kc + 1 < KC) transform();

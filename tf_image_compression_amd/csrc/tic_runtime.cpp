@@ -731,6 +731,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.xbuf = ln.xbuf;
       a.flags = ln.cflags;
       a.ctl = ln.ctl;
+      if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
                                   st))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);

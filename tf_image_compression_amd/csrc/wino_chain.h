@@ -56,6 +56,8 @@ struct ChainArgs {
   float* xbuf;          // border exchange [nl-1][n*R][4 sides][8 px][64] f32
   unsigned* flags;      // [nl-1][n*R] epoch flags
   unsigned* ctl;        // [0] ticket, [1] done count, [2] epoch, [3] error (poll timeout)
+  int probe;            // timing probes only (TIC_CHAIN_PROBE; results invalid unless 0):
+                        // 1 = no hand-off at all, 2 = publish but do not wait / read
 };
 
 namespace chain {
@@ -221,10 +223,14 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(l, s + PF, nb);
         }
+        // keep each weight load PF steps (48 MFMAs) ahead of its use: without the fence the
+        // scheduler sinks the loads next to their consumers inside the chunk
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = mfma4(av[s % (PF + 1)][nb][t], V[nu][t], acc[nu][nb]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (kc + 1 < KC) transform();
@@ -317,7 +323,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
     __syncthreads();
 
     // ---- hand-off: publish this region's border, then read the neighbours' ----
-    if (R > 1) {
+    if (R > 1 && a.probe != 1) {
       const size_t g = (size_t)nimg * R + reg;
       float* const xb = a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C);
 #pragma unroll
@@ -331,7 +337,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
       __syncthreads();
       if (tid == 0) __hip_atomic_store(&a.flags[(size_t)l * nR + g], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // wait for the (up to 8) neighbours' flags of this layer
-      if (tid < 9 && tid != 4) {
+      if (a.probe == 0 && tid < 9 && tid != 4) {
         const int nry = ry + tid / 3 - 1, nrx = rx + tid % 3 - 1;
         if (nry >= 0 && nry < a.rh && nrx >= 0 && nrx < a.rw) {
           const unsigned* f = &a.flags[(size_t)l * nR + (size_t)nimg * R + nry * a.rw + nrx];
@@ -356,7 +362,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
         else hy = hp - 28, hx = 8;
         const int gy = oy0 + hy, gx = ox0 + hx;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        if (a.probe == 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
           const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
           const int ny = hy & 7, nx = hx & 7;  // pixel inside the neighbour region
           int side, idx;
