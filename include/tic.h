@@ -203,6 +203,13 @@ int tic_memset_device(tic_handle* h, void* d_ptr, int value, size_t bytes);
 /* Make `waiter`'s stream wait for all work enqueued so far on `signaler`'s stream (same
  * device): chains a codec handle and an rmbe handle without a host synchronisation. */
 int tic_stream_wait(tic_handle* waiter, tic_handle* signaler);
+/* Named dependencies (slot 0..7): tic_event_record marks the point reached so far on h's
+ * stream; tic_stream_wait_event makes `waiter`'s stream wait for the last mark of that
+ * slot on `signaler` (no-op if never recorded).  Lets a pipeline wait for exactly the
+ * work that last used a buffer (e.g. the rmbe pass of image i-2 before the codec of
+ * image i reuses its stitch buffer) instead of everything enqueued so far. */
+int tic_event_record(tic_handle* h, int slot);
+int tic_stream_wait_event(tic_handle* waiter, tic_handle* signaler, int slot);
 
 /* CRC-32C (Castagnoli) of n bytes, continuing `crc` (0 to start).  Host only.  Used by the
  * TensorFlow checkpoint reader that replaces tf.train.Saver.restore (utils/utils.py:84-93):

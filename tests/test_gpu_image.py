@@ -178,3 +178,33 @@ def test_get_encoded_distribution_tool(codecs, tmp_path):
     sym = c0.encode(pats)
     ref, _ = np.histogram(sym, [0, 1, 2])
     assert np.array_equal(freq, ref.astype(np.float64))
+
+
+def test_image_pipeline_back_to_back(codecs):
+    """Three images enqueued back to back (no host synchronisation): the codec of image
+    i+1 overlaps the rmbe passes of image i through the two stitch buffers and named
+    events; results equal images decoded one at a time."""
+    from tf_image_compression_amd.image_codec import ImageCodec
+    c0, cr, _, _ = codecs
+    H, W = 200, 330
+    imgs = [_image(H, W, 30 + k) for k in range(3)]
+    ic = ImageCodec(c0, cr)
+    ref = [ic.decode_image(ic.encode_image(im), H, W, post_filter=True) for im in imgs]
+    eh, ew, ec = c0.code_shape
+    n = ic.num_patches(H, W)
+    d_img = [c0.alloc(H * W * 3) for _ in imgs]
+    d_sym = [c0.alloc(n * eh * ew * ec) for _ in imgs]
+    d_out = [c0.alloc(H * W * 3) for _ in imgs]
+    for d, im in zip(d_img, imgs):
+        d.upload(im)
+    for k in range(3):
+        ic.roundtrip_device(d_img[k], H, W, d_sym[k], d_out[k], post_filter=True)
+    ic.synchronize()
+    for k in range(3):
+        assert np.array_equal(d_out[k].download((H, W, 3), np.uint8), ref[k])
+    # the same output buffer reused for consecutive images: the last write wins
+    for k in (0, 1, 2):
+        ic.roundtrip_device(d_img[k], H, W, d_sym[0], d_out[0], post_filter=True)
+    ic.synchronize()
+    assert np.array_equal(d_out[0].download((H, W, 3), np.uint8), ref[2])
+    ic.close()

@@ -356,7 +356,7 @@ def test_fused_tail_bit_identical(lib_codec, monkeypatch, model_id, P):
         u0, f0 = codec.decode(idx, return_float=True)
         codec.set_option("fuse_tail", 1)
         outs = []
-        for v in ("0", "1"):
+        for v in ("0", "1", "2", "3"):
             monkeypatch.setenv("TIC_DEC10_VARIANT", v)
             outs.append(codec.decode(idx, return_float=True))
     finally:

@@ -67,6 +67,8 @@ SIGNATURES = [
     ("tic_sse_u8_device", C.c_int, [vp, vp, vp, C.c_size_t, vp]),
     ("tic_memset_device", C.c_int, [vp, vp, C.c_int, C.c_size_t]),
     ("tic_stream_wait", C.c_int, [vp, vp]),
+    ("tic_event_record", C.c_int, [vp, C.c_int]),
+    ("tic_stream_wait_event", C.c_int, [vp, vp, C.c_int]),
     ("tic_crc32c", C.c_uint32, [C.c_char_p, C.c_size_t, C.c_uint32]),
     # entropy coder (host only)
     ("tic_rc_last_error", C.c_char_p, []),

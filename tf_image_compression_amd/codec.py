@@ -252,6 +252,14 @@ class Codec:
         """Order this handle's stream after everything enqueued so far on ``other``'s."""
         check(lib().tic_stream_wait(self._h, other._h), "tic_stream_wait")
 
+    def record(self, slot: int) -> None:
+        """Mark the work enqueued so far on this handle's stream as event ``slot`` (0..7)."""
+        check(lib().tic_event_record(self._h, slot), "tic_event_record")
+
+    def wait_event(self, other: "Codec", slot: int) -> None:
+        """Order this handle's stream after ``other``'s last mark of ``slot`` (if any)."""
+        check(lib().tic_stream_wait_event(self._h, other._h, slot), "tic_stream_wait_event")
+
     # ------------------------------------------------------------------ lifetime
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

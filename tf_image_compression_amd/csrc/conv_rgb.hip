@@ -124,12 +124,19 @@ bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int vari
 template <int C1, int C0>
 static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
   dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n);
-  if (variant == 0) hipLaunchKernelGGL((dec10_kernel<C1, C0, false>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((dec10_kernel<C1, C0, true>), grid, dim3(256), 0, s, a);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2>), grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5>), grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5>), grid, dim3(256), 0, s, a); break;
+    default: return false;
+  }
   return true;
 }
 
-int dec10_variants() { return 2; }  // decode_0 weights: 0 scalar loads, 1 LDS
+// decode_0 weights: scalar loads (0, 2) or LDS (1, 3); decode_1 weight prefetch 2 (0, 1)
+// or 5 (2, 3) steps ahead — all bit-identical
+int dec10_variants() { return 4; }
 
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {
   if (variant < 0 || variant >= dec10_variants()) return false;

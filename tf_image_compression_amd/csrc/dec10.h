@@ -25,8 +25,10 @@
 namespace tic {
 
 // WSH: decode_0's weights staged in LDS (broadcast ds_read_b128) or read with wave-uniform
-// addresses from memory (scalar loads), as the two convT_rgb_valu kernels do.
-template <int C1, int C0, bool WSH>
+// addresses from memory (scalar loads), as the two convT_rgb_valu kernels do.  PF: how many
+// K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles, so PF = 2
+// covers only an idle-chip L2 hit; PF = 5 covers a loaded one).  Neither changes results.
+template <int C1, int C0, bool WSH, int PF = 2>
 __global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
   constexpr int TA = 4;                            // decode_1 input rows (x 16 columns)
   constexpr int PSX = C1 + 8, KC = C1 / 16, C4 = C1 / 4;
@@ -50,7 +52,7 @@ __global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
 
   // ---- decode_1 weights from L2 (generic packing), prefetched PF steps ahead ----
-  constexpr int PF = 2, NSTEP = 9 * KC;
+  constexpr int NSTEP = 9 * KC;
   const float* __restrict__ wl = a.wp1 + (size_t)(lg * C0 + li) * 4;
   auto wglob = [&](int s, int nb) -> f32x4 {
     const int tap = s / KC, kc = s % KC;

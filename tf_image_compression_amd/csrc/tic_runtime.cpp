@@ -372,6 +372,8 @@ struct tic_handle {
   void* win_out = nullptr;
   size_t win_out_bytes = 0;
   hipEvent_t ev_dep = nullptr;  // tic_stream_wait
+  hipEvent_t ev_slot[8] = {};   // tic_event_record / tic_stream_wait_event
+  bool ev_slot_set[8] = {};
   std::vector<void*> user_allocs;
   int tune_reps = 0;  // > 0 while tic_autotune runs
   int num_cus = 256;
@@ -1109,6 +1111,8 @@ void tic_destroy(tic_handle* h) {
   if (h->win_in) (void)hipFree(h->win_in);
   if (h->win_out) (void)hipFree(h->win_out);
   if (h->ev_dep) (void)hipEventDestroy(h->ev_dep);
+  for (auto& e : h->ev_slot)
+    if (e) (void)hipEventDestroy(e);
   for (void* p : h->user_allocs) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1727,7 +1731,7 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
       auto iv = l.tuned_var.find(n);
       int v = iv != l.tuned_var.end() ? iv->second : 0;
       if (const char* t = getenv("TIC_DEC10_VARIANT")) v = atoi(t);
-      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s>", d.cin, d.cout, tf[v == 1]);
+      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s,%d>", d.cin, d.cout, tf[v & 1], v >= 2 ? 5 : 2);
     }
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
@@ -2017,6 +2021,26 @@ int tic_stream_wait(tic_handle* waiter, tic_handle* signaler) {
   if (!signaler->ev_dep) HIP_TRY(hipEventCreateWithFlags(&signaler->ev_dep, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(signaler->ev_dep, signaler->stream));
   HIP_TRY(hipStreamWaitEvent(waiter->stream, signaler->ev_dep, 0));
+  return TIC_OK;
+}
+
+int tic_event_record(tic_handle* h, int slot) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  if (slot < 0 || slot >= 8) return fail(TIC_EINVAL, "event slot %d out of range [0, 8)", slot);
+  HIP_TRY(hipSetDevice(h->device));
+  if (!h->ev_slot[slot]) HIP_TRY(hipEventCreateWithFlags(&h->ev_slot[slot], hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(h->ev_slot[slot], h->stream));
+  h->ev_slot_set[slot] = true;
+  return TIC_OK;
+}
+
+int tic_stream_wait_event(tic_handle* waiter, tic_handle* signaler, int slot) {
+  if (!waiter || !signaler) return fail(TIC_EINVAL, "null handle");
+  if (slot < 0 || slot >= 8) return fail(TIC_EINVAL, "event slot %d out of range [0, 8)", slot);
+  if (waiter->device != signaler->device) return fail(TIC_EINVAL, "handles on different devices");
+  if (!signaler->ev_slot_set[slot]) return TIC_OK;
+  HIP_TRY(hipSetDevice(waiter->device));
+  HIP_TRY(hipStreamWaitEvent(waiter->stream, signaler->ev_slot[slot], 0));
   return TIC_OK;
 }
 

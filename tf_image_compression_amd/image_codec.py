@@ -6,9 +6,16 @@ The reference does the image plumbing on the host between ``sess.run`` calls:
 block-effect post-filter ``rmbe.rmbe`` (submit/2/rmbe/rmbe.py:15-111) and
 ``np.around(...).astype(np.uint8)`` (submit/2/decoder.py:176; decode.py:249).  Here every
 one of those steps is a kernel on the codec's stream (image_ops.hip), the rmbe network
-runs on its own handle, and the two streams are chained with an event
-(``Codec.wait_for``) instead of a host synchronisation.  Host memory is touched only to
-upload the uint8 image / symbols and download the result.
+runs on its own handle, and the two streams are chained with events instead of a host
+synchronisation.  Host memory is touched only to upload the uint8 image / symbols and
+download the result.
+
+Pipelining (BASELINE configs[4]): the stitched float image that the post-filter works on
+in place alternates between two buffers, and the codec stream waits only for the rmbe
+pass that last used the buffer it is about to overwrite (image i-2, a named event), not
+for everything the rmbe stream has queued.  So the codec of image i+1 runs while the rmbe
+passes of image i do — two streams, two networks, one GPU.  Callers that reuse their own
+output buffer for consecutive images are ordered by the same rule (see decode_image_device).
 """
 from __future__ import annotations
 
@@ -20,10 +27,13 @@ from .codec import Codec, DeviceBuffer
 class ImageCodec:
     """``codec``: a model_N Codec; ``post``: optional rmbe Codec (TIC_MODEL_RMBE)."""
 
+    NSLOT = 2  # stitch buffers in flight (codec of image i+1 beside rmbe of image i)
+
     def __init__(self, codec: Codec, post: Codec | None = None):
         self.codec = codec
         self.post = post
         self._bufs: dict[str, DeviceBuffer] = {}
+        self._slot = 0
 
     # ------------------------------------------------------------------ geometry
     def grid(self, H: int, W: int) -> tuple[int, int]:
@@ -60,16 +70,32 @@ class ImageCodec:
         P = self.codec.patch_size
         n = self.num_patches(H, W)
         d_f = self._buf("patches_f32", n * P * P * 3 * 4)
-        d_img = self._buf("image_f32", H * W * 3 * 4)
-        self.codec.decode_device(d_sym, n, None, d_f)
-        self.codec.patches_to_image_device(d_f, H, W, P, d_img)
         if post_filter and self.post is not None:
-            self.post.wait_for(self.codec)
+            k = self._slot
+            self._slot = (k + 1) % self.NSLOT
+            d_img = self._buf(f"image_f32_{k}", H * W * 3 * 4)
+            self.codec.decode_device(d_sym, n, None, d_f)
+            # the rmbe pass that last filtered this stitch buffer (and wrote the previous
+            # output from it) must be done before the codec overwrites it
+            self.codec.wait_event(self.post, k)
+            self.codec.patches_to_image_device(d_f, H, W, P, d_img)
+            self.codec.record(k)
+            self.post.wait_event(self.codec, k)
             self.post.rmbe_image_device(d_img, H, W)
             self.post.round_u8_device(d_img, H * W * 3, d_out)
-            self.codec.wait_for(self.post)  # later codec work may reuse the buffers
+            self.post.record(k)
         else:
+            # no post-filter: everything on the codec stream, ordered after any pending
+            # post-filter work that still reads a stitch buffer
+            d_img = self._buf("image_f32_0", H * W * 3 * 4)
+            if self.post is not None:
+                self.codec.wait_event(self.post, 0)
+            self.codec.decode_device(d_sym, n, None, d_f)
+            self.codec.patches_to_image_device(d_f, H, W, P, d_img)
             self.codec.round_u8_device(d_img, H * W * 3, d_out)
+            if self.post is not None:
+                self.codec.record(0)
+                self.post.wait_event(self.codec, 0)  # a later filtered image reuses slot 0
 
     def roundtrip_device(self, d_img: DeviceBuffer, H: int, W: int, d_sym: DeviceBuffer, d_out: DeviceBuffer,
                          post_filter: bool = True) -> None:
