@@ -26,181 +26,263 @@ namespace tic {
 
 // WSH: decode_0's weights staged in LDS (broadcast ds_read_b128) or read with wave-uniform
 // addresses from memory (scalar loads), as the two convT_rgb_valu kernels do.  PF: how many
-// K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles, so PF = 2
-// covers only an idle-chip L2 hit; PF = 5 covers a loaded one).  Neither changes results.
-template <int C1, int C0, bool WSH, int PF = 2>
-__global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
-  constexpr int TA = 4;                            // decode_1 input rows (x 16 columns)
-  constexpr int PSX = C1 + 8, KC = C1 / 16, C4 = C1 / 4;
-  constexpr int LRX = TA + 1, LCX = 17;
-  constexpr int XT = LRX * LCX * PSX;              // decode_1 input tile (floats)
-  constexpr int TH = 2 * TA, TW = 32;              // decode_0 input positions
-  constexpr int PSY = C0 + 4, LRY = TH + 1, LCY = TW + 1;
-  constexpr int YT = LRY * LCY * PSY;              // decode_0 input tile incl. halo (floats)
-  constexpr int OT = 2 * TH * 2 * TW * 3;          // decode_0 output staging (floats)
+// K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles).  PROBE:
+// timing experiments only (1 = decode_1 on the VALU, 2 = no decode_0 work; results invalid).
+// None of WSH / PF changes results.
+template <int C1, int C0, bool WSH, int PF, int PROBE>
+struct Dec10 {
+  static constexpr int TA = 4;                      // decode_1 input rows (x 16 columns)
+  static constexpr int PSX = C1 + 8, KC = C1 / 16, C4 = C1 / 4;
+  static constexpr int LRX = TA + 1, LCX = 17;
+  static constexpr int XT = LRX * LCX * PSX;        // decode_1 input tile (floats)
+  static constexpr int TH = 2 * TA, TW = 32;        // decode_0 input positions
+  static constexpr int PSY = C0 + 4, LRY = TH + 1, LCY = TW + 1;
+  static constexpr int YT = LRY * LCY * PSY;        // decode_0 input tile incl. halo (floats)
+  static constexpr int OT = 2 * TH * 2 * TW * 3;    // decode_0 output staging (floats)
+  static constexpr int NB = C0 / 16;
+  static constexpr int NSTEP = 9 * KC;
+  static constexpr int NSTAGE = LRX * LCX * C4;
+  static constexpr int NIT = (NSTAGE + 255) / 256;
+  static constexpr int SMEM = XT + YT + (WSH ? 27 * C0 : 4);
   static_assert(OT <= XT && C1 % 16 == 0 && C0 % 16 == 0, "tile");
-  constexpr int NB = C0 / 16;
-  __shared__ __attribute__((aligned(16))) float smem[XT + YT + (WSH ? 27 * C0 : 4)];
-  float* const xt = smem;
-  float* const yt = smem + XT;
-  float* const wsh = smem + XT + YT;
 
-  const int tid = threadIdx.x;
-  const int q0 = blockIdx.x * 16, m0 = blockIdx.y * TA, nimg = blockIdx.z;
-  const int H = a.H, W = a.W;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // decode_1 input row of this wave
-  const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
-
-  // ---- decode_1 weights from L2 (generic packing), prefetched PF steps ahead ----
-  constexpr int NSTEP = 9 * KC;
-  const float* __restrict__ wl = a.wp1 + (size_t)(lg * C0 + li) * 4;
-  auto wglob = [&](int s, int nb) -> f32x4 {
+  __device__ static f32x4 wglob(const Dec10Args& a, int s, int nb, int li, int lg) {
     const int tap = s / KC, kc = s % KC;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC + kc) * 4 * C0 * 4 + nb * 64);
-  };
-  f32x4 av[PF + 1][NB];
-#pragma unroll
-  for (int p = 0; p < PF; ++p)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) av[p][nb] = wglob(p, nb);
-  if (WSH) rgb_out_load_weights<C0, 256>(a.rgb.wraw, wsh, tid);
+    return *reinterpret_cast<const f32x4*>(a.wp1 + (size_t)(lg * C0 + li) * 4 + (size_t)(tap * KC + kc) * 4 * C0 * 4 +
+                                           nb * 64);
+  }
 
-  // ---- 1. stage decode_1's input tile ----
-  constexpr int NSTAGE = LRX * LCX * C4;
-  constexpr int NIT = (NSTAGE + 255) / 256;
-  {
-    f32x4 tmp[NIT];
+  // decode_1's input rows m0-1 .. m0+3, columns q0-1 .. q0+15 (zero outside) into registers
+  __device__ static void issue(const Dec10Args& a, f32x4 (&pre)[NIT], int q0, int m0, int nimg, int tid) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int e = i * 256 + tid;
-      tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      pre[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (e < NSTAGE) {
         const int c4 = e % C4, pe = e / C4, col = pe % LCX, row = pe / LCX;
         const int iy = m0 - 1 + row, ix = q0 - 1 + col;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-          tmp[i] = *reinterpret_cast<const f32x4*>(a.in + ((size_t)(nimg * H + iy) * W + ix) * C1 + c4 * 4);
+        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+          pre[i] = *reinterpret_cast<const f32x4*>(a.in + ((size_t)(nimg * a.H + iy) * a.W + ix) * C1 + c4 * 4);
       }
     }
+  }
+  __device__ static void land(float* xt, const f32x4 (&pre)[NIT], int tid) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int e = i * 256 + tid;
-      if (e < NSTAGE) *reinterpret_cast<f32x4*>(&xt[(e / C4) * PSX + (e % C4) * 4]) = tmp[i];
-    }
-  }
-  __syncthreads();
-
-  // ---- 2. interior: conv3x3_kernel<MODE_T2>'s step order, one input row per wave ----
-  f32x4 acc[4][NB];
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[p][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto load_b = [&](int s) -> f32x4 {
-    const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
-    const int lp = (wave + 1 - (ky == 2)) * LCX + li + 1 - (kx == 2);
-    return *reinterpret_cast<const f32x4*>(&xt[lp * PSX + kc * 16 + lg * 4]);
-  };
-  f32x4 bq[2];
-  bq[0] = load_b(0);
-#pragma unroll
-  for (int s = 0; s < NSTEP; ++s) {
-    const int tap = s / KC, ky = tap / 3, kx = tap % 3;
-    const int c = s & 1;
-    if (s + PF < NSTEP) {
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
-    }
-    if (s + 1 < NSTEP) bq[c ^ 1] = load_b(s + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    const int ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[ph][nb] = mfma4(av[s % (PF + 1)][nb][t], bq[c][t], acc[ph][nb]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int py = p >> 1, px = p & 1;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int co = nb * 16 + lg * 4;
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
-      f32x4 v = acc[p][nb];
-      v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
-      v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
-      v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
-      v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
-      *reinterpret_cast<f32x4*>(&yt[((1 + 2 * wave + py) * LCY + 1 + 2 * li + px) * PSY + co]) = v;
+      if (e < NSTAGE) *reinterpret_cast<f32x4*>(&xt[(e / C4) * PSX + (e % C4) * 4]) = pre[i];
     }
   }
 
-  // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
-  //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
-  //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
-  //         q0-1, rows m0-1 .. m0+3: taps 1, 4, 7; lane j = input row m0-1+j, j <= 4) ----
-  if (wave < 2) {
-    const bool row = wave == 0;
-    f32x4 ha[3 * KC][NB];
+  // One tile, its input already in xt (and a barrier behind it): decode_1 by MFMA into yt,
+  // the halo, decode_0 on the VALU, the output.  av holds the first PF weight steps on
+  // entry; with `again`, they are reloaded for the next tile right after the K loop.
+  __device__ static void tile(const Dec10Args& a, float* xt, float* yt, const float* wsh, f32x4 (&av)[PF + 1][NB],
+                              int q0, int m0, int nimg, bool again) {
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // decode_1 input row of this wave
+    const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
+
+    // ---- 2. interior: conv3x3_kernel<MODE_T2>'s step order, one input row per wave ----
+    f32x4 acc[4][NB];
 #pragma unroll
-    for (int ti = 0; ti < 3; ++ti)
+    for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc)
+      for (int nb = 0; nb < NB; ++nb) acc[p][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto load_b = [&](int s) -> f32x4 {
+      const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
+      const int lp = (wave + 1 - (ky == 2)) * LCX + li + 1 - (kx == 2);
+      return *reinterpret_cast<const f32x4*>(&xt[lp * PSX + kc * 16 + lg * 4]);
+    };
+    f32x4 bq[2];
+    bq[0] = load_b(0);
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) ha[ti * KC + kc][nb] = wglob(((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb);
-    f32x4 hacc[2][NB];  // [0]: phase 2 (row) / phase 1 (column); [1]: phase 3
+    for (int s = 0; s < NSTEP; ++s) {
+      const int tap = s / KC, ky = tap / 3, kx = tap % 3;
+      const int c = s & 1;
+      if (s + PF < NSTEP) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ti = 0; ti < 3; ++ti) {
-      const int tap = (row ? 3 : 1) + ti * (row ? 1 : 3);
-      const int q = tap == 4 ? 1 : 0;
-      int lp;
-      if (row) lp = li + 1 - (tap == 5);  // input row m0-1 (LDS row 0), column q0+li (-1 for tap 5)
-      else lp = min(max(li - (tap == 7), 0), LRX - 1) * LCX;  // input column q0-1 (LDS column 0)
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(&xt[lp * PSX + kc * 16 + lg * 4]);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
+        for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(a, s + PF, nb, li, lg);
       }
+      if (s + 1 < NSTEP) bq[c ^ 1] = load_b(s + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const int ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          if constexpr (PROBE == 1) acc[ph][nb][t] += av[s % (PF + 1)][nb][t] * bq[c][t];
+          else acc[ph][nb] = mfma4(av[s % (PF + 1)][nb][t], bq[c][t], acc[ph][nb]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (again) {  // the next tile's first weight steps (the same weights) fly from here
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) av[p][nb] = wglob(a, p, nb, li, lg);
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int p = 0; p < 4; ++p) {
+      const int py = p >> 1, px = p & 1;
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         const int co = nb * 16 + lg * 4;
-        int ry, cy;
-        bool use;
-        if (row) {
-          ry = 0, cy = 1 + 2 * li + q, use = true;
-        } else {
-          ry = q ? 2 * li : 2 * li - 1, cy = 0, use = q ? li <= 4 : (li >= 1 && li <= 4);
-        }
-        if (!use) continue;
-        const bool inside = 2 * m0 - 1 + ry >= 0 && 2 * q0 - 1 + cy >= 0;
         const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
-        f32x4 v = hacc[q][nb];
-        v.x = inside ? fmaxf(__fadd_rn(v.x, bb.x), 0.f) : 0.f;
-        v.y = inside ? fmaxf(__fadd_rn(v.y, bb.y), 0.f) : 0.f;
-        v.z = inside ? fmaxf(__fadd_rn(v.z, bb.z), 0.f) : 0.f;
-        v.w = inside ? fmaxf(__fadd_rn(v.w, bb.w), 0.f) : 0.f;
-        *reinterpret_cast<f32x4*>(&yt[(ry * LCY + cy) * PSY + co]) = v;
+        f32x4 v = acc[p][nb];
+        v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
+        v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
+        v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
+        v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
+        *reinterpret_cast<f32x4*>(&yt[((1 + 2 * wave + py) * LCY + 1 + 2 * li + px) * PSY + co]) = v;
       }
+    }
+
+    // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
+    //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
+    //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
+    //         q0-1, rows m0-1 .. m0+3: taps 1, 4, 7; lane j = input row m0-1+j, j <= 4) ----
+    if (wave < 2) {
+      const bool row = wave == 0;
+      f32x4 ha[3 * KC][NB];
+#pragma unroll
+      for (int ti = 0; ti < 3; ++ti)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            ha[ti * KC + kc][nb] = wglob(a, ((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb, li, lg);
+      f32x4 hacc[2][NB];  // [0]: phase 2 (row) / phase 1 (column); [1]: phase 3
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ti = 0; ti < 3; ++ti) {
+        const int tap = (row ? 3 : 1) + ti * (row ? 1 : 3);
+        const int q = tap == 4 ? 1 : 0;
+        int lp;
+        if (row) lp = li + 1 - (tap == 5);  // input row m0-1 (LDS row 0), column q0+li (-1 for tap 5)
+        else lp = min(max(li - (tap == 7), 0), LRX - 1) * LCX;  // input column q0-1 (LDS column 0)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const f32x4 b = *reinterpret_cast<const f32x4*>(&xt[lp * PSX + kc * 16 + lg * 4]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const int co = nb * 16 + lg * 4;
+          int ry, cy;
+          bool use;
+          if (row) {
+            ry = 0, cy = 1 + 2 * li + q, use = true;
+          } else {
+            ry = q ? 2 * li : 2 * li - 1, cy = 0, use = q ? li <= 4 : (li >= 1 && li <= 4);
+          }
+          if (!use) continue;
+          const bool inside = 2 * m0 - 1 + ry >= 0 && 2 * q0 - 1 + cy >= 0;
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
+          f32x4 v = hacc[q][nb];
+          v.x = inside ? fmaxf(__fadd_rn(v.x, bb.x), 0.f) : 0.f;
+          v.y = inside ? fmaxf(__fadd_rn(v.y, bb.y), 0.f) : 0.f;
+          v.z = inside ? fmaxf(__fadd_rn(v.z, bb.z), 0.f) : 0.f;
+          v.w = inside ? fmaxf(__fadd_rn(v.w, bb.w), 0.f) : 0.f;
+          *reinterpret_cast<f32x4*>(&yt[(ry * LCY + cy) * PSY + co]) = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- 4. decode_0 on the VALU; output tile staged in the dead decode_1 input tile ----
+    const int r = tid / TW, c = tid % TW;
+    float acc3[4][3] = {};
+    if constexpr (PROBE == 2) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
+    else rgb_out_fma<C0, PSY, LCY>(&yt[((r + 1) * LCY + (c + 1)) * PSY], WSH ? wsh : a.rgb.wraw, acc3);
+    rgb_out_epilogue(a.rgb, acc3, xt, 2 * TW * 3, r, c);
+    __syncthreads();
+    rgb_out_store<TH, TW, 256>(a.rgb, xt, tid, 2 * m0, 2 * q0, nimg);
+  }
+};
+
+// One launch per tile (grid = tiles).
+template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0>
+__global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
+  using D = Dec10<C1, C0, WSH, PF, PROBE>;
+  __shared__ __attribute__((aligned(16))) float smem[D::SMEM];
+  float* const xt = smem;
+  float* const yt = smem + D::XT;
+  float* const wsh = smem + D::XT + D::YT;
+  const int tid = threadIdx.x;
+  const int q0 = blockIdx.x * 16, m0 = blockIdx.y * D::TA, nimg = blockIdx.z;
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
+  f32x4 av[PF + 1][D::NB];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int nb = 0; nb < D::NB; ++nb) av[p][nb] = D::wglob(a, p, nb, li, lg);
+  if (WSH) rgb_out_load_weights<C0, 256>(a.rgb.wraw, wsh, tid);
+  {  // ---- 1. stage decode_1's input tile ----
+    f32x4 pre[D::NIT];
+    D::issue(a, pre, q0, m0, nimg, tid);
+    D::land(xt, pre, tid);
   }
   __syncthreads();
+  D::tile(a, xt, yt, wsh, av, q0, m0, nimg, false);
+}
 
-  // ---- 4. decode_0 on the VALU; output tile staged in the dead decode_1 input tile ----
-  const int r = tid / TW, c = tid % TW;
-  float acc3[4][3] = {};
-  rgb_out_fma<C0, PSY, LCY>(&yt[((r + 1) * LCY + (c + 1)) * PSY], WSH ? wsh : a.rgb.wraw, acc3);
-  rgb_out_epilogue(a.rgb, acc3, xt, 2 * TW * 3, r, c);
-  __syncthreads();
-  rgb_out_store<TH, TW, 256>(a.rgb, xt, tid, 2 * m0, 2 * q0, nimg);
+// Persistent, software-pipelined: grid = min(tiles, 2 x CUs); each workgroup walks tiles
+// t, t + grid, ...  The next tile's input loads are issued into registers as soon as this
+// tile's input has landed in LDS, and decode_1's first weight steps right after this
+// tile's K loop, so both fly while this tile computes and writes back (the one-shot
+// launch pays the staging latency once per 4x16 tile).  Same arithmetic, same order:
+// bit-identical to dec10_kernel.
+template <int C1, int C0, bool WSH, int PF>
+__global__ void __launch_bounds__(256, 2) dec10_persist_kernel(const Dec10Args a, int ntx, int nty, int ntiles) {
+  using D = Dec10<C1, C0, WSH, PF, 0>;
+  __shared__ __attribute__((aligned(16))) float smem[D::SMEM];
+  float* const xt = smem;
+  float* const yt = smem + D::XT;
+  float* const wsh = smem + D::XT + D::YT;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  auto coords = [&](int tt, int& q0, int& m0, int& nimg) {
+    q0 = (tt % ntx) * 16;
+    m0 = ((tt / ntx) % nty) * D::TA;
+    nimg = tt / (ntx * nty);
+  };
+  f32x4 pre[D::NIT];
+  {
+    int q0, m0, nimg;
+    coords(t, q0, m0, nimg);
+    D::issue(a, pre, q0, m0, nimg, tid);
+  }
+  f32x4 av[PF + 1][D::NB];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int nb = 0; nb < D::NB; ++nb) av[p][nb] = D::wglob(a, p, nb, li, lg);
+  if (WSH) rgb_out_load_weights<C0, 256>(a.rgb.wraw, wsh, tid);
+  for (; t < ntiles; t += gridDim.x) {
+    D::land(xt, pre, tid);
+    __syncthreads();
+    const bool more = t + (int)gridDim.x < ntiles;
+    if (more) {
+      int q1, m1, n1;
+      coords(t + gridDim.x, q1, m1, n1);
+      D::issue(a, pre, q1, m1, n1, tid);
+    }
+    int q0, m0, nimg;
+    coords(t, q0, m0, nimg);
+    D::tile(a, xt, yt, wsh, av, q0, m0, nimg, more);
+    __syncthreads();  // the output stage (xt) is read by every thread before the next landing
+  }
 }
 
 }  // namespace tic

@@ -685,6 +685,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.rgb.out_u8 = d_rgb;
       a.rgb.out_f32 = d_f32;
       a.rgb.H = a.rgb.W = last_l.h_in;
+      a.rgb.num_cus = h->num_cus;
+      a.rgb.grid_cap = h->persist_grid;
       for (int c = 0; c < 3; ++c) {
         a.rgb.mean[c] = h->mean[c];
         a.rgb.std[c] = h->std[c];
@@ -1731,7 +1733,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
       auto iv = l.tuned_var.find(n);
       int v = iv != l.tuned_var.end() ? iv->second : 0;
       if (const char* t = getenv("TIC_DEC10_VARIANT")) v = atoi(t);
-      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s,%d>", d.cin, d.cout, tf[v & 1], v >= 2 ? 5 : 2);
+      snprintf(buf, sizeof buf, "%s<%d,%d,%s,%d>", (v & 4) ? "dec10_persist_kernel" : "dec10_kernel", d.cin, d.cout,
+               tf[v & 1], (v & 2) ? 5 : 2);
     }
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
