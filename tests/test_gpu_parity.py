@@ -359,10 +359,7 @@ def test_fused_tail_bit_identical(lib_codec, monkeypatch, model_id, P):
         for v in ("0", "1", "2", "3", "4", "5", "6", "7"):
             monkeypatch.setenv("TIC_DEC10_VARIANT", v)
             outs.append(codec.decode(idx, return_float=True))
-            if int(v) >= 4:  # persistent: also with a grid of 5 workgroups walking many tiles
-                codec.set_option("persist_grid", 5)
-                outs.append(codec.decode(idx, return_float=True))
-                codec.set_option("persist_grid", 0)
+
     finally:
         codec.set_option("fuse_tail", 0)
     for u1, f1 in outs:

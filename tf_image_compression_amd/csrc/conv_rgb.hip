@@ -121,26 +121,18 @@ bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int vari
   return false;
 }
 
-template <int C1, int C0, bool WSH, int PF>
-static void dec10_persist(const Dec10Args& a, int n, hipStream_t s) {
-  const int ntx = (a.W + 15) / 16, nty = (a.H + 3) / 4, ntiles = ntx * nty * n;
-  int grid = std::min(ntiles, 2 * std::max(1, a.rgb.num_cus));
-  if (a.rgb.grid_cap > 0) grid = std::min(grid, a.rgb.grid_cap);
-  hipLaunchKernelGGL((dec10_persist_kernel<C1, C0, WSH, PF>), dim3(grid), dim3(256), 0, s, a, ntx, nty, ntiles);
-}
-
 template <int C1, int C0>
 static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
-  dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n);
+  dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n), grid8((a.W + 15) / 16, (a.H + 7) / 8, n);
   switch (variant) {
     case 0: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2>), grid, dim3(256), 0, s, a); break;
     case 1: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2>), grid, dim3(256), 0, s, a); break;
     case 2: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5>), grid, dim3(256), 0, s, a); break;
     case 3: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5>), grid, dim3(256), 0, s, a); break;
-    case 4: dec10_persist<C1, C0, false, 2>(a, n, s); break;
-    case 5: dec10_persist<C1, C0, true, 2>(a, n, s); break;
-    case 6: dec10_persist<C1, C0, false, 5>(a, n, s); break;
-    case 7: dec10_persist<C1, C0, true, 5>(a, n, s); break;
+    case 4: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 0, 8>), grid8, dim3(512), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2, 0, 8>), grid8, dim3(512), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5, 0, 8>), grid8, dim3(512), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5, 0, 8>), grid8, dim3(512), 0, s, a); break;
     // timing probes (TIC_DEC10_VARIANT only; results invalid): decode_1 on the VALU / no decode_0
     case 8: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1>), grid, dim3(256), 0, s, a); break;
     case 9: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2>), grid, dim3(256), 0, s, a); break;
@@ -150,8 +142,7 @@ static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
 }
 
 // decode_0 weights: scalar loads (even) or LDS (odd); decode_1 weight prefetch 2 or 5
-// steps ahead; one launch per tile (0-3) or persistent + software-pipelined (4-7) — all
-// bit-identical
+// steps ahead; tiles of 4 (0-3) or 8 (4-7) decode_1 input rows — all bit-identical
 int dec10_variants() { return 8; }
 
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {

@@ -29,9 +29,10 @@ namespace tic {
 // K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles).  PROBE:
 // timing experiments only (1 = decode_1 on the VALU, 2 = no decode_0 work; results invalid).
 // None of WSH / PF changes results.
-template <int C1, int C0, bool WSH, int PF, int PROBE>
+template <int C1, int C0, bool WSH, int PF, int PROBE, int TA_ = 4>
 struct Dec10 {
-  static constexpr int TA = 4;                      // decode_1 input rows (x 16 columns)
+  static constexpr int TA = TA_;                    // decode_1 input rows (x 16 columns), one per wave
+  static constexpr int NT = 64 * TA;                // threads: one decode_0 input position each
   static constexpr int PSX = C1 + 8, KC = C1 / 16, C4 = C1 / 4;
   static constexpr int LRX = TA + 1, LCX = 17;
   static constexpr int XT = LRX * LCX * PSX;        // decode_1 input tile (floats)
@@ -42,9 +43,10 @@ struct Dec10 {
   static constexpr int NB = C0 / 16;
   static constexpr int NSTEP = 9 * KC;
   static constexpr int NSTAGE = LRX * LCX * C4;
-  static constexpr int NIT = (NSTAGE + 255) / 256;
+  static constexpr int NIT = (NSTAGE + NT - 1) / NT;
   static constexpr int SMEM = XT + YT + (WSH ? 27 * C0 : 4);
-  static_assert(OT <= XT && C1 % 16 == 0 && C0 % 16 == 0, "tile");
+  static constexpr bool OUT_IN_XT = OT <= XT;       // output staging: the dead input tile, else yt
+  static_assert(OT <= YT && C1 % 16 == 0 && C0 % 16 == 0, "tile");
 
   __device__ static f32x4 wglob(const Dec10Args& a, int s, int nb, int li, int lg) {
     const int tap = s / KC, kc = s % KC;
@@ -56,7 +58,7 @@ struct Dec10 {
   __device__ static void issue(const Dec10Args& a, f32x4 (&pre)[NIT], int q0, int m0, int nimg, int tid) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int e = i * 256 + tid;
+      const int e = i * NT + tid;
       pre[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (e < NSTAGE) {
         const int c4 = e % C4, pe = e / C4, col = pe % LCX, row = pe / LCX;
@@ -69,7 +71,7 @@ struct Dec10 {
   __device__ static void land(float* xt, const f32x4 (&pre)[NIT], int tid) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int e = i * 256 + tid;
+      const int e = i * NT + tid;
       if (e < NSTAGE) *reinterpret_cast<f32x4*>(&xt[(e / C4) * PSX + (e % C4) * 4]) = pre[i];
     }
   }
@@ -141,7 +143,7 @@ struct Dec10 {
     // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
     //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
     //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
-    //         q0-1, rows m0-1 .. m0+3: taps 1, 4, 7; lane j = input row m0-1+j, j <= 4) ----
+    //         q0-1, rows m0-1 .. m0+TA-1: taps 1, 4, 7; lane j = input row m0-1+j, j <= TA) ----
     if (wave < 2) {
       const bool row = wave == 0;
       f32x4 ha[3 * KC][NB];
@@ -183,7 +185,7 @@ struct Dec10 {
           if (row) {
             ry = 0, cy = 1 + 2 * li + q, use = true;
           } else {
-            ry = q ? 2 * li : 2 * li - 1, cy = 0, use = q ? li <= 4 : (li >= 1 && li <= 4);
+            ry = q ? 2 * li : 2 * li - 1, cy = 0, use = q ? li <= TA : (li >= 1 && li <= TA);
           }
           if (!use) continue;
           const bool inside = 2 * m0 - 1 + ry >= 0 && 2 * q0 - 1 + cy >= 0;
@@ -198,21 +200,26 @@ struct Dec10 {
     }
     __syncthreads();
 
-    // ---- 4. decode_0 on the VALU; output tile staged in the dead decode_1 input tile ----
+    // ---- 4. decode_0 on the VALU; output tile staged in the dead decode_1 input tile (or,
+    //         when it is too small, in yt once every thread has read its inputs) ----
     const int r = tid / TW, c = tid % TW;
     float acc3[4][3] = {};
     if constexpr (PROBE == 2) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
     else rgb_out_fma<C0, PSY, LCY>(&yt[((r + 1) * LCY + (c + 1)) * PSY], WSH ? wsh : a.rgb.wraw, acc3);
-    rgb_out_epilogue(a.rgb, acc3, xt, 2 * TW * 3, r, c);
+    float* const ot = OUT_IN_XT ? xt : yt;
+    if constexpr (!OUT_IN_XT) __syncthreads();
+    rgb_out_epilogue(a.rgb, acc3, ot, 2 * TW * 3, r, c);
     __syncthreads();
-    rgb_out_store<TH, TW, 256>(a.rgb, xt, tid, 2 * m0, 2 * q0, nimg);
+    rgb_out_store<TH, TW, NT>(a.rgb, ot, tid, 2 * m0, 2 * q0, nimg);
   }
 };
 
-// One launch per tile (grid = tiles).
-template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0>
-__global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
-  using D = Dec10<C1, C0, WSH, PF, PROBE>;
+// One workgroup per tile of TA x 16 decode_1 input positions (TA waves): TA = 4 runs two
+// workgroups per CU, TA = 8 one of twice the size (half the halo re-read and per-tile
+// overhead per position).
+template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0, int TA = 4>
+__global__ void __launch_bounds__(64 * TA, 8 / TA) dec10_kernel(const Dec10Args a) {
+  using D = Dec10<C1, C0, WSH, PF, PROBE, TA>;
   __shared__ __attribute__((aligned(16))) float smem[D::SMEM];
   float* const xt = smem;
   float* const yt = smem + D::XT;
@@ -225,7 +232,7 @@ __global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
   for (int p = 0; p < PF; ++p)
 #pragma unroll
     for (int nb = 0; nb < D::NB; ++nb) av[p][nb] = D::wglob(a, p, nb, li, lg);
-  if (WSH) rgb_out_load_weights<C0, 256>(a.rgb.wraw, wsh, tid);
+  if (WSH) rgb_out_load_weights<C0, D::NT>(a.rgb.wraw, wsh, tid);
   {  // ---- 1. stage decode_1's input tile ----
     f32x4 pre[D::NIT];
     D::issue(a, pre, q0, m0, nimg, tid);
@@ -233,56 +240,6 @@ __global__ void __launch_bounds__(256, 2) dec10_kernel(const Dec10Args a) {
   }
   __syncthreads();
   D::tile(a, xt, yt, wsh, av, q0, m0, nimg, false);
-}
-
-// Persistent, software-pipelined: grid = min(tiles, 2 x CUs); each workgroup walks tiles
-// t, t + grid, ...  The next tile's input loads are issued into registers as soon as this
-// tile's input has landed in LDS, and decode_1's first weight steps right after this
-// tile's K loop, so both fly while this tile computes and writes back (the one-shot
-// launch pays the staging latency once per 4x16 tile).  Same arithmetic, same order:
-// bit-identical to dec10_kernel.
-template <int C1, int C0, bool WSH, int PF>
-__global__ void __launch_bounds__(256, 2) dec10_persist_kernel(const Dec10Args a, int ntx, int nty, int ntiles) {
-  using D = Dec10<C1, C0, WSH, PF, 0>;
-  __shared__ __attribute__((aligned(16))) float smem[D::SMEM];
-  float* const xt = smem;
-  float* const yt = smem + D::XT;
-  float* const wsh = smem + D::XT + D::YT;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
-  auto coords = [&](int tt, int& q0, int& m0, int& nimg) {
-    q0 = (tt % ntx) * 16;
-    m0 = ((tt / ntx) % nty) * D::TA;
-    nimg = tt / (ntx * nty);
-  };
-  f32x4 pre[D::NIT];
-  {
-    int q0, m0, nimg;
-    coords(t, q0, m0, nimg);
-    D::issue(a, pre, q0, m0, nimg, tid);
-  }
-  f32x4 av[PF + 1][D::NB];
-#pragma unroll
-  for (int p = 0; p < PF; ++p)
-#pragma unroll
-    for (int nb = 0; nb < D::NB; ++nb) av[p][nb] = D::wglob(a, p, nb, li, lg);
-  if (WSH) rgb_out_load_weights<C0, 256>(a.rgb.wraw, wsh, tid);
-  for (; t < ntiles; t += gridDim.x) {
-    D::land(xt, pre, tid);
-    __syncthreads();
-    const bool more = t + (int)gridDim.x < ntiles;
-    if (more) {
-      int q1, m1, n1;
-      coords(t + gridDim.x, q1, m1, n1);
-      D::issue(a, pre, q1, m1, n1, tid);
-    }
-    int q0, m0, nimg;
-    coords(t, q0, m0, nimg);
-    D::tile(a, xt, yt, wsh, av, q0, m0, nimg, more);
-    __syncthreads();  // the output stage (xt) is read by every thread before the next landing
-  }
 }
 
 }  // namespace tic

@@ -1733,8 +1733,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
       auto iv = l.tuned_var.find(n);
       int v = iv != l.tuned_var.end() ? iv->second : 0;
       if (const char* t = getenv("TIC_DEC10_VARIANT")) v = atoi(t);
-      snprintf(buf, sizeof buf, "%s<%d,%d,%s,%d>", (v & 4) ? "dec10_persist_kernel" : "dec10_kernel", d.cin, d.cout,
-               tf[v & 1], (v & 2) ? 5 : 2);
+      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s,%d,0,%d>", d.cin, d.cout, tf[v & 1], (v & 2) ? 5 : 2,
+               (v & 4) ? 8 : 4);
     }
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name

@@ -31,6 +31,6 @@ if __name__ == "__main__":
         child(int(sys.argv[1]), int(sys.argv[2]))
     else:
         for n in (32, 64):
-            for v in (0, 1, 4, 5, 6, 7, 8, 9):
+            for v in (0, 2, 4, 5, 6, 7):
                 env = dict(os.environ, TIC_DEC10_VARIANT=str(v))
                 subprocess.run([sys.executable, __file__, str(v), str(n)], env=env, check=True, timeout=120)
