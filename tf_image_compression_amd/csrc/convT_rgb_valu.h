@@ -29,32 +29,11 @@
 
 namespace tic {
 
-// The (phase, offset) pairs of the last layer: offset d = (dy, dx) in {0,-1}^2 feeds the
-// phases p = 2 py + px with py = 0 or dy = 0, and px = 0 or dx = 0, through tap
-// ky = py ? 1 : (dy ? 2 : 0), kx likewise.  Per offset the phases are paired for v_pk_fma:
-//   (0,0): (0,1) (2,3)   (0,-1): (0,2)   (-1,0): (0,1)   (-1,-1): 0 alone.
-// Weights are packed (tic_runtime.cpp pack_rgb_out_valu) so that for every offset and input
-// channel the operands of one step sit next to each other: [off][ci][pair][co][2] then
-// [off][ci][co] for the unpaired phase — an aligned SGPR pair feeds each v_pk_fma directly.
-struct RgbValuPlan {
-  static constexpr int NPAIR[4] = {2, 1, 1, 0};
-  static constexpr int NSINGLE[4] = {0, 0, 0, 1};
-  static constexpr int PH[4][4] = {{0, 1, 2, 3}, {0, 2, -1, -1}, {0, 1, -1, -1}, {0, -1, -1, -1}};
-  // floats per input channel of each offset, and the offset's base (in units of CIN floats)
-  static constexpr int PER_CI[4] = {12, 6, 6, 3};
-  static constexpr int BASE[4] = {0, 12, 18, 24};
-};
-
 // acc[phase][co] += the 9 (phase, offset) products of one input position.  `self` points at
 // the position in an LDS tile of pitch PS floats per position and LC positions per row, so
-// that offset (-1, 0) is self - LC*PS and (0, -1) is self - PS.  `w`: the packed weights.
-// Per offset the ci loop is outermost and all of that offset's (phase, channel) chains
-// advance together (independent chains in flight instead of one dependent chain at a
-// time).  Every output's own order — offsets (0,0), (0,-1), (-1,0), (-1,-1), Cin ascending
-// within each — is fixed, so all VALU-form kernels are bit-identical.
+// that offset (-1, 0) is self - LC*PS and (0, -1) is self - PS.  `w` is [3][3][3][CIN].
 template <int CIN, int PS, int LC>
 __device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, float (&acc)[4][3]) {
-  using PL = RgbValuPlan;
   constexpr int C4 = CIN / 4;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
@@ -70,39 +49,42 @@ __device__ __forceinline__ void rgb_out_fma(const float* self, const float* __re
       x[4 * c4 + 2] = v.z;
       x[4 * c4 + 3] = v.w;
     }
-    const int npair = PL::NPAIR[off];
-    f32x2 s2[2][3];
+    // phases using this offset, paired so one packed fma (v_pk_fma_f32) advances two
+    // outputs' chains by one step each — every output's own fma order is unchanged
+    int ph[4], np = 0;
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int p = 0; p < 4; ++p)
+      if (!((dy != 0 && (p >> 1) == 1) || (dx != 0 && (p & 1) == 1))) ph[np++] = p;
 #pragma unroll
-      for (int co = 0; co < 3; ++co)
-        if (k < npair) s2[k][co] = f32x2{acc[PL::PH[off][2 * k]][co], acc[PL::PH[off][2 * k + 1]][co]};
-    const float* wo = w + PL::BASE[off] * CIN;
+    for (int k = 0; k + 1 < np; k += 2) {
+      const int pa = ph[k], pb = ph[k + 1];
+      const int kya = (pa >> 1) ? 1 : (dy == 0 ? 0 : 2), kxa = (pa & 1) ? 1 : (dx == 0 ? 0 : 2);
+      const int kyb = (pb >> 1) ? 1 : (dy == 0 ? 0 : 2), kxb = (pb & 1) ? 1 : (dx == 0 ? 0 : 2);
 #pragma unroll
-    for (int ci = 0; ci < CIN; ++ci) {
-      const float* wc = wo + ci * PL::PER_CI[off];
-      const f32x2 xx = {x[ci], x[ci]};
+      for (int co = 0; co < 3; ++co) {
+        const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
+        const float* wb = w + ((kyb * 3 + kxb) * 3 + co) * CIN;
+        f32x2 s2 = {acc[pa][co], acc[pb][co]};
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int co = 0; co < 3; ++co)
-          if (k < npair) {
-            const f32x2 ww = *reinterpret_cast<const f32x2*>(wc + 2 * (k * 3 + co));
-            s2[k][co] = __builtin_elementwise_fma(xx, ww, s2[k][co]);
-          }
-      if (PL::NSINGLE[off]) {
-#pragma unroll
-        for (int co = 0; co < 3; ++co) acc[PL::PH[off][0]][co] = fmaf(x[ci], wc[co], acc[PL::PH[off][0]][co]);
+        for (int ci = 0; ci < CIN; ++ci) {
+          const f32x2 xx = {x[ci], x[ci]};
+          const f32x2 ww = {wa[ci], wb[ci]};
+          s2 = __builtin_elementwise_fma(xx, ww, s2);
+        }
+        acc[pa][co] = s2.x;
+        acc[pb][co] = s2.y;
       }
     }
+    if (np & 1) {
+      const int pa = ph[np - 1];
+      const int kya = (pa >> 1) ? 1 : (dy == 0 ? 0 : 2), kxa = (pa & 1) ? 1 : (dx == 0 ? 0 : 2);
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+      for (int co = 0; co < 3; ++co) {
+        const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
 #pragma unroll
-      for (int co = 0; co < 3; ++co)
-        if (k < npair) {
-          acc[PL::PH[off][2 * k]][co] = s2[k][co].x;
-          acc[PL::PH[off][2 * k + 1]][co] = s2[k][co].y;
-        }
+        for (int ci = 0; ci < CIN; ++ci) acc[pa][co] = fmaf(x[ci], wa[ci], acc[pa][co]);
+      }
+    }
   }
 }
 
@@ -174,11 +156,11 @@ __device__ __forceinline__ void rgb_out_store(const RgbOutArgs& a, const float* 
   }
 }
 
-// The packed 27 x CIN weights into LDS (16-byte aligned source: a device allocation).
+// The raw [3][3][3][CIN] kernel into LDS (16-byte aligned source: a device allocation).
 template <int CIN, int NT>
-__device__ __forceinline__ void rgb_out_load_weights(const float* __restrict__ wvalu, float* wsh, int tid) {
+__device__ __forceinline__ void rgb_out_load_weights(const float* __restrict__ wraw, float* wsh, int tid) {
   for (int e = tid; e < 27 * CIN / 4; e += NT)
-    reinterpret_cast<f32x4*>(wsh)[e] = reinterpret_cast<const f32x4*>(wvalu)[e];
+    reinterpret_cast<f32x4*>(wsh)[e] = reinterpret_cast<const f32x4*>(wraw)[e];
 }
 
 template <int CIN, int TW>
@@ -225,7 +207,7 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_kernel(const RgbOutArgs a)
 
   const int r = tid / TW, c = tid % TW;
   float acc[4][3] = {};
-  rgb_out_fma<CIN, PS, LC>(&lds[((r + 1) * LC + (c + 1)) * PS], a.wvalu, acc);
+  rgb_out_fma<CIN, PS, LC>(&lds[((r + 1) * LC + (c + 1)) * PS], a.wraw, acc);
   __syncthreads();  // input tile no longer needed: reuse LDS for the output tile
   rgb_out_epilogue(a, acc, lds, 2 * TW * 3, r, c);
   __syncthreads();
@@ -281,7 +263,7 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_persist_kernel(const RgbOu
   int t = blockIdx.x;
   if (t >= ntiles) return;
   issue(t);
-  rgb_out_load_weights<CIN, 256>(a.wvalu, wsh, tid);
+  rgb_out_load_weights<CIN, 256>(a.wraw, wsh, tid);
   for (; t < ntiles; t += gridDim.x) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {

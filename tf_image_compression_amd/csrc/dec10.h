@@ -205,7 +205,7 @@ struct Dec10 {
     const int r = tid / TW, c = tid % TW;
     float acc3[4][3] = {};
     if constexpr (PROBE == 2) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
-    else rgb_out_fma<C0, PSY, LCY>(&yt[((r + 1) * LCY + (c + 1)) * PSY], WSH ? wsh : a.rgb.wvalu, acc3);
+    else rgb_out_fma<C0, PSY, LCY>(&yt[((r + 1) * LCY + (c + 1)) * PSY], WSH ? wsh : a.rgb.wraw, acc3);
     float* const ot = OUT_IN_XT ? xt : yt;
     if constexpr (!OUT_IN_XT) __syncthreads();
     rgb_out_epilogue(a.rgb, acc3, ot, 2 * TW * 3, r, c);
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(64 * TA, 8 / TA) dec10_kernel(const Dec10Args 
   for (int p = 0; p < PF; ++p)
 #pragma unroll
     for (int nb = 0; nb < D::NB; ++nb) av[p][nb] = D::wglob(a, p, nb, li, lg);
-  if (WSH) rgb_out_load_weights<C0, D::NT>(a.rgb.wvalu, wsh, tid);
+  if (WSH) rgb_out_load_weights<C0, D::NT>(a.rgb.wraw, wsh, tid);
   {  // ---- 1. stage decode_1's input tile ----
     f32x4 pre[D::NIT];
     D::issue(a, pre, q0, m0, nimg, tid);

@@ -58,7 +58,7 @@ struct RgbOutArgs {
   const float* in;     // [N,H,W,Cin]
   const float* wp;     // dense sub-pixel form: [4 off][Cin/16][16 rows][4][4]
   const float* wp2;    // scatter form: [2 rb][Cin/16][4 g][16 rows][4 t]
-  const float* wvalu;  // VALU form: pair-packed (pack_rgb_out_valu / rgb_out_fma), 27 x Cin floats
+  const float* wraw;   // VALU form: the TF kernel as-is, [3][3][3][Cin]
   const float* bias;   // [3]
   uint8_t* out_u8;     // [N,2H,2W,3] or nullptr
   float* out_f32;      // [N,2H,2W,3] or nullptr
@@ -75,7 +75,7 @@ struct Dec10Args {
   const float* w1raw;  // decode_1 TF kernel as-is, [3][3][C0][C1]
   const float* b1;     // [C0]
   int H, W;            // decode_1 input size (decode_0's input is 2H x 2W)
-  RgbOutArgs rgb;      // decode_0: wvalu, bias, normalisation, outputs; rgb.H/W = 2H/2W
+  RgbOutArgs rgb;      // decode_0: wraw, bias, normalisation, outputs; rgb.H/W = 2H/2W
 };
 
 typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);

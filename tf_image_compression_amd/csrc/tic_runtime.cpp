@@ -298,37 +298,6 @@ void pack_rgb_out(const float* k, int cin, std::vector<float>* wp) {
   }
 }
 
-// Last layer, VALU form (convT_rgb_valu.h RgbValuPlan): per input offset (0,0), (0,-1),
-// (-1,0), (-1,-1) and input channel, the weight pairs of the offset's phase pairs then the
-// unpaired phase's weights: [off][ci][pair][co][2] / [off][ci][co]; from [3,3,3,Cin].
-void pack_rgb_out_valu(const float* k, int cin, std::vector<float>* wp) {
-  static const int npair[4] = {2, 1, 1, 0}, ph[4][4] = {{0, 1, 2, 3}, {0, 2, -1, -1}, {0, 1, -1, -1}, {0, -1, -1, -1}};
-  static const int per_ci[4] = {12, 6, 6, 3}, base[4] = {0, 12, 18, 24};
-  wp->assign((size_t)27 * cin, 0.f);
-  auto tap = [](int p, int dy, int dx, int* ky, int* kx) {
-    *ky = (p >> 1) ? 1 : (dy == 0 ? 0 : 2);
-    *kx = (p & 1) ? 1 : (dx == 0 ? 0 : 2);
-  };
-  for (int off = 0; off < 4; ++off) {
-    const int dy = -(off >> 1), dx = -(off & 1);
-    for (int ci = 0; ci < cin; ++ci) {
-      float* dst = wp->data() + (size_t)base[off] * cin + (size_t)ci * per_ci[off];
-      int ky, kx;
-      if (npair[off]) {
-        for (int kk = 0; kk < npair[off]; ++kk)
-          for (int co = 0; co < 3; ++co)
-            for (int e = 0; e < 2; ++e) {
-              tap(ph[off][2 * kk + e], dy, dx, &ky, &kx);
-              dst[2 * (kk * 3 + co) + e] = k[(((size_t)ky * 3 + kx) * 3 + co) * cin + ci];
-            }
-      } else {
-        tap(ph[off][0], dy, dx, &ky, &kx);
-        for (int co = 0; co < 3; ++co) dst[co] = k[(((size_t)ky * 3 + kx) * 3 + co) * cin + ci];
-      }
-    }
-  }
-}
-
 // Last layer, scatter form: [2 rb][Cin/16][4 g][16 rows][4 t], row 16 rb + rr = 3 tap + co.
 void pack_rgb_out_scatter(const float* k, int cin, std::vector<float>* wp) {
   const int KC = cin / 16;
@@ -353,7 +322,7 @@ struct LayerRT {
   bool has_k = false, has_b = false;
   float* d_w = nullptr;
   float* d_w2 = nullptr;  // alternate packing (last layer: scatter form)
-  float* d_w3 = nullptr;  // last layer: VALU-form packing; layer L-2: its TF kernel (fused tail halo)
+  float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
   float* d_ww = nullptr;  // stride-1 layers: Winograd-packed U (conv3x3_wino.h)
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
@@ -711,7 +680,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.w1raw = lay.d_w3;
       a.b1 = lay.d_b;
       a.H = a.W = lay.h_in;
-      a.rgb.wvalu = last_l.d_w3;
+      a.rgb.wraw = last_l.d_w3;
       a.rgb.bias = last_l.d_b;
       a.rgb.out_u8 = d_rgb;
       a.rgb.out_f32 = d_f32;
@@ -813,7 +782,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.in = src;
       a.wp = lay.d_w;
       a.wp2 = lay.d_w2;
-      a.wvalu = lay.d_w3;
+      a.wraw = lay.d_w3;
       a.num_cus = h->num_cus;
       a.grid_cap = h->persist_grid;
       a.bias = lay.d_b;
@@ -1232,10 +1201,8 @@ int tic_finalize(tic_handle* h) {
       pack_rgb_out_scatter(l.k.data(), l.def.cin, &w2);
       HIP_TRY(hipMalloc((void**)&l.d_w2, w2.size() * sizeof(float)));
       HIP_TRY(hipMemcpy(l.d_w2, w2.data(), w2.size() * sizeof(float), hipMemcpyHostToDevice));
-      std::vector<float> w3;
-      pack_rgb_out_valu(l.k.data(), l.def.cin, &w3);
-      HIP_TRY(hipMalloc((void**)&l.d_w3, w3.size() * sizeof(float)));
-      HIP_TRY(hipMemcpy(l.d_w3, w3.data(), w3.size() * sizeof(float), hipMemcpyHostToDevice));
+      HIP_TRY(hipMalloc((void**)&l.d_w3, l.k.size() * sizeof(float)));
+      HIP_TRY(hipMemcpy(l.d_w3, l.k.data(), l.k.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     HIP_TRY(hipMalloc((void**)&l.d_w, wp.size() * sizeof(float)));
     HIP_TRY(hipMemcpy(l.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
