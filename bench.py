@@ -55,6 +55,8 @@ def parse():
                     help="tuning state (tic_tuning_export) to replay instead of tuning: 'auto' = the "
                          "committed tools/tune/<config>.json when its source stamp matches (else tune), "
                          "'none' = always tune, PATH = load if present and matching, else tune and save")
+    ap.add_argument("--trace-only", action="store_true",
+                    help="stop after the timed steps (for rocprofv3 timelines of the steady state)")
     ap.add_argument("--pmc-plan", default=None,
                     help="PMC mode (tools/pmc_box.sh): tune exactly as the bench does, then run --steps "
                          "steps on ONE lane at the per-lane batch (deterministic dispatch order), write "
@@ -340,6 +342,13 @@ def main():
     elapsed = time.perf_counter() - t0
     wall1 = time.time()
     t_max = comm.allreduce_max(elapsed)
+    if args.trace_only:
+        if rank == 0:
+            print(json.dumps({"trace_only": True, "ms_per_step": t_max * 1e3 / args.steps,
+                              "launches_per_lane": sum(1 for k in codec.layer_kernels(lane_b) if k)}), flush=True)
+        comm.close()
+        codec.close()
+        return
 
     # per-rank stats -> the one RCCL all-gather (SSE of the last reconstruction)
     rec = d_rgb.download(x.shape, np.uint8)

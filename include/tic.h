@@ -155,8 +155,15 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
                        int cout, const float* w_host, const float* b_host, const float* d_res, float* d_out);
 
 /* The handle's HIP stream (hipStream_t as void*), e.g. to enqueue an RCCL collective
- * behind the codec's kernels. */
+ * behind the codec's kernels.  Work enqueued there is ordered before every later codec
+ * call: from this call on the handle's execution lanes fork from the stream at every call
+ * (see tic_stream_external). */
 int tic_get_stream(tic_handle* h, void** stream);
+/* Declare whether the caller may have work of its own pending on the handle's stream
+ * (1, the state after tic_get_stream) or synchronises everything it enqueues there before
+ * the next codec call (0): then the lanes fork from the stream only after the handle's own
+ * copies / glue kernels, and each lane starts its next batch as soon as it is free. */
+int tic_stream_external(tic_handle* h, int on);
 
 /* Device info string (name, CUs, arch) for logs. */
 int tic_device_info(tic_handle* h, char* buf, int len);

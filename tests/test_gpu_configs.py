@@ -238,3 +238,35 @@ def test_graph_replay_after_workspace_growth():
         assert np.array_equal(d_idx.download(ref_idx.shape, np.uint8), ref_idx)
         assert np.array_equal(d_rgb.download(x8.shape, np.uint8), ref_rgb)
         c.set_option("graph", 0)
+
+
+@pytest.mark.parametrize("decouple", [0, 1])
+def test_lane_decoupling_orders_stream_work(decouple):
+    """Lanes fork from the handle stream only when it has new work (option "decouple"):
+    glue work enqueued on the handle stream between two codec calls must still see the
+    first call's results (the histogram reads d_idx before the second call overwrites it)
+    and the second call must see the caller's new input."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.image_codec import symbol_histogram
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    P, n = 64, 12
+    x1, x2 = structured_patches(n, P, seed=801), structured_patches(n, P, seed=802)
+    with Codec(0, synthetic_params(0), SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
+        c.set_option("decouple", decouple)
+        c.set_option("streams", 3)
+        ref1, ref2 = c.encode(x1), c.encode(x2)
+        eh, ew, ec = c.code_shape
+        d_in, d_idx, d_rgb = c.alloc(x1.nbytes), c.alloc(n * eh * ew * ec), c.alloc(x1.nbytes)
+        d_cnt = c.alloc(16)
+        for _ in range(3):
+            d_in.upload(x1)
+            c.codec_device(d_in, n, d_idx, d_rgb)
+            c.memset_device(d_cnt, 0, 16)
+            c.histogram_device(d_idx, n * eh * ew * ec, 2, d_cnt)  # reads call 1's symbols
+            d_in.upload(x2)
+            c.codec_device(d_in, n, d_idx, d_rgb)
+            got1 = d_cnt.download((2,), np.uint64)
+            c.synchronize()
+            assert np.array_equal(got1.astype(np.int64), np.histogram(ref1, [0, 1, 2])[0])
+            assert np.array_equal(d_idx.download(ref2.shape, np.uint8), ref2)
+        c.set_option("streams", 2)

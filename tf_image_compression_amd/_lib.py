@@ -59,6 +59,7 @@ SIGNATURES = [
     ("tic_conv3x3_device", C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      f32p, f32p, vp, vp]),
     ("tic_get_stream", C.c_int, [vp, C.POINTER(vp)]),
+    ("tic_stream_external", C.c_int, [vp, C.c_int]),
     ("tic_image_to_patches_device", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
     ("tic_patches_to_image_device", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, vp]),
     ("tic_rmbe_image_device", C.c_int, [vp, vp, C.c_int, C.c_int]),

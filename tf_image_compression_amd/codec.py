@@ -172,6 +172,10 @@ class Codec:
         check(lib().tic_get_stream(self._h, C.byref(s)), "tic_get_stream")
         return s
 
+    def stream_external(self, on: bool) -> None:
+        """Whether work of the caller's own may be pending on stream_ptr() (tic_stream_external)."""
+        check(lib().tic_stream_external(self._h, int(bool(on))), "tic_stream_external")
+
     def synchronize(self) -> None:
         check(lib().tic_synchronize(self._h), "tic_synchronize")
 

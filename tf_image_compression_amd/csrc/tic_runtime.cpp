@@ -383,6 +383,13 @@ struct tic_handle {
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
+  // Lane scheduling: lanes join into `stream` after every call, but wait on it (fork) only
+  // when something else was enqueued there since their last fork ("decouple"), so lane k's
+  // next batch starts as soon as lane k is free instead of after the slowest lane.
+  bool decouple = true;
+  bool stream_dirty = true;     // non-lane work enqueued on `stream` since the last fork
+  bool external_stream = false; // the caller holds the raw stream (tic_get_stream): always fork
+  bool force_fork = false;      // tuning / graph capture: every call forks
   struct GraphKey {
     const void *in, *idx, *rgb;
     int n, nlanes;
@@ -393,6 +400,10 @@ struct tic_handle {
   std::map<GraphKey, hipGraphExec_t> graphs;  // captured encode->decode sequences
   bool rmbe() const { return model_id == TIC_MODEL_RMBE; }
 };
+
+// Anything enqueued on h->stream outside the lanes (copies, image glue, waits) must be seen
+// by the lanes' next fork: it may produce their inputs or still read their outputs.
+static void touch(tic_handle* h) { h->stream_dirty = true; }
 
 // Key of a layer's tuned-tiling map: the batch size, per stride-1 form (each form has its
 // own candidate set, so switching the form never reuses the other form's choice).
@@ -889,11 +900,6 @@ size_t code_elems(const tic_handle* h) {
 template <typename F>
 int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
   const int k = allow_split ? std::min(h->nlanes, m) : 1;
-  if (k < 2) {
-    int rc = ensure_ws(h, h->lanes[0], m);
-    if (rc) return rc;
-    return body(h->lanes[0], 0, m);
-  }
   int part[4], off[4];
   for (int i = 0, o = 0; i < k; ++i) {
     part[i] = m / k + (i < m % k ? 1 : 0);
@@ -904,11 +910,17 @@ int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
     int rc = ensure_ws(h, h->lanes[i], part[i]);
     if (rc) return rc;
   }
-  HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-  for (int i = 1; i < k; ++i) HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
+  const bool fork = !h->decouple || h->stream_dirty || h->external_stream || h->force_fork || h->tune_reps > 0;
+  if (fork) {
+    HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+    for (int i = 0; i < k; ++i) HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
+    // lanes that sit this call out are behind the fork too the next time they run
+    for (int i = k; i < 4; ++i) HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
+    h->stream_dirty = false;
+  }
   int rc = TIC_OK;
   for (int i = 0; i < k && !rc; ++i) rc = body(h->lanes[i], off[i], part[i]);
-  for (int i = 1; i < k; ++i) {
+  for (int i = 0; i < k; ++i) {
     HIP_TRY(hipEventRecord(h->ev_join[i], h->lanes[i].stream));
     HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join[i], 0));
   }
@@ -1064,8 +1076,9 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   else h->fuse_tail = kFuseTailDefault;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
+  if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-  for (int i = 1; i < 4 && e == hipSuccess; ++i) {
+  for (int i = 0; i < 4 && e == hipSuccess; ++i) {
     e = hipStreamCreateWithFlags(&h->lanes[i].stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming);
   }
@@ -1074,7 +1087,6 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
     delete h;
     return fail(TIC_EHIP, "stream/event creation: %s", hipGetErrorString(e));
   }
-  h->lanes[0].stream = h->stream;
   *out = h;
   return TIC_OK;
 }
@@ -1098,7 +1110,7 @@ void tic_destroy(tic_handle* h) {
     if (ln.cflags) (void)hipFree(ln.cflags);
     if (ln.ctl) (void)hipFree(ln.ctl);
   }
-  for (int i = 1; i < 4; ++i) {
+  for (int i = 0; i < 4; ++i) {
     if (h->lanes[i].stream) {
       (void)hipStreamSynchronize(h->lanes[i].stream);
       (void)hipStreamDestroy(h->lanes[i].stream);
@@ -1251,6 +1263,7 @@ int tic_device_free(tic_handle* h, void* dptr) {
 
 int tic_memcpy_h2d(tic_handle* h, void* dst, const void* src, size_t bytes) {
   if (!h) return fail(TIC_EINVAL, "null handle");
+  touch(h);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return TIC_OK;
@@ -1258,6 +1271,7 @@ int tic_memcpy_h2d(tic_handle* h, void* dst, const void* src, size_t bytes) {
 
 int tic_memcpy_d2h(tic_handle* h, void* dst, const void* src, size_t bytes) {
   if (!h) return fail(TIC_EINVAL, "null handle");
+  touch(h);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return TIC_OK;
@@ -1304,7 +1318,9 @@ int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    h->force_fork = true;  // every lane must join the capture through the fork event
     rc = codec_dev(h, d_patches, n, d_idx, d_rgb);
+    h->force_fork = false;
     hipError_t e = hipStreamEndCapture(h->stream, &g);
     if (rc) {
       if (g) (void)hipGraphDestroy(g);
@@ -1318,6 +1334,7 @@ int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_
     return TIC_OK;
   }
   HIP_TRY(hipGraphLaunch(it->second, h->stream));
+  touch(h);  // the graph's lane work ran inside h->stream's order
   return TIC_OK;
 }
 
@@ -1357,6 +1374,12 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->fuse_tail = value != 0;
     return TIC_OK;
   }
+  if (k == "decouple") {  // lanes fork from the handle stream only when it has new work
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->decouple = value != 0;
+    h->stream_dirty = true;
+    return TIC_OK;
+  }
   if (k == "chain") {  // stride-1 runs in one wino_chain_kernel launch (Winograd form only)
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
@@ -1392,10 +1415,12 @@ int tic_encode(tic_handle* h, const uint8_t* patches, int n, uint8_t* idx_out, f
   if ((rc = ensure(&h->st_in, &h->st_in_bytes, in_b))) return rc;
   if ((rc = ensure(&h->st_out, &h->st_out_bytes, ce))) return rc;
   if (preact_out && (rc = ensure(&h->st_out2, &h->st_out2_bytes, ce * 4))) return rc;
+  touch(h);
   HIP_TRY(hipMemcpyAsync(h->st_in, patches, in_b, hipMemcpyHostToDevice, h->stream));
   rc = encode_dev(h, (const uint8_t*)h->st_in, n, (uint8_t*)h->st_out, preact_out ? (float*)h->st_out2 : nullptr,
                   Prof{nullptr});
   if (rc) return rc;
+  touch(h);
   HIP_TRY(hipMemcpyAsync(idx_out, h->st_out, ce, hipMemcpyDeviceToHost, h->stream));
   if (preact_out) HIP_TRY(hipMemcpyAsync(preact_out, h->st_out2, ce * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1413,10 +1438,12 @@ int tic_decode(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb_out, float
   if (rgb_out && (rc = ensure(&h->st_out, &h->st_out_bytes, px))) return rc;
   if (f32_out && (rc = ensure(&h->st_out2, &h->st_out2_bytes, px * 4))) return rc;
   // symbols must be < Q (the LUT beyond Q is zero-filled; the reference would produce NaN/inf)
+  touch(h);
   HIP_TRY(hipMemcpyAsync(h->st_in, idx, ce, hipMemcpyHostToDevice, h->stream));
   rc = decode_dev(h, (const uint8_t*)h->st_in, n, rgb_out ? (uint8_t*)h->st_out : nullptr,
                   f32_out ? (float*)h->st_out2 : nullptr, Prof{nullptr});
   if (rc) return rc;
+  touch(h);
   if (rgb_out) HIP_TRY(hipMemcpyAsync(rgb_out, h->st_out, px, hipMemcpyDeviceToHost, h->stream));
   if (f32_out) HIP_TRY(hipMemcpyAsync(f32_out, h->st_out2, px * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1432,9 +1459,11 @@ int tic_rmbe(tic_handle* h, const float* windows, int n, float* out) {
   const size_t b = (size_t)n * h->P * h->P * 3 * sizeof(float);
   if ((rc = ensure(&h->st_in, &h->st_in_bytes, b))) return rc;
   if ((rc = ensure(&h->st_out2, &h->st_out2_bytes, b))) return rc;
+  touch(h);
   HIP_TRY(hipMemcpyAsync(h->st_in, windows, b, hipMemcpyHostToDevice, h->stream));
   rc = rmbe_dev(h, (const float*)h->st_in, n, (float*)h->st_out2, Prof{nullptr});
   if (rc) return rc;
+  touch(h);
   HIP_TRY(hipMemcpyAsync(out, h->st_out2, b, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return check_chain_error(h);
@@ -1566,6 +1595,12 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   HIP_TRY(ev0.create());
   HIP_TRY(ev1.create());
   hipEvent_t t0 = ev0.e, t1 = ev1.e;
+  struct ForceFork {  // events on h->stream bracket whole steps only if every call forks
+    tic_handle* h;
+    bool was;
+    ~ForceFork() { h->force_fork = was; }
+  } ff{h, h->force_fork};
+  h->force_fork = true;
   auto step = [&]() {
     return h->rmbe() ? rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr})
                      : codec_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, (uint8_t*)d_out);
@@ -1905,6 +1940,7 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.pad_x = same_pad(kind, W);
   a.num_cus = h->num_cus;
   a.grid_cap = h->persist_grid;
+  touch(h);
   e->fn(a, n, h->stream);
   int rc = check_launch();
   hipError_t se = hipStreamSynchronize(h->stream);
@@ -1916,6 +1952,14 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
 int tic_get_stream(tic_handle* h, void** stream) {
   if (!h || !stream) return fail(TIC_EINVAL, "null argument");
   *stream = (void*)h->stream;
+  h->external_stream = true;  // the caller may enqueue anything there from now on
+  return TIC_OK;
+}
+
+int tic_stream_external(tic_handle* h, int on) {
+  if (!h) return fail(TIC_EINVAL, "null handle");
+  h->external_stream = on != 0;
+  h->stream_dirty = true;  // whatever happened there so far is seen by the next fork
   return TIC_OK;
 }
 
@@ -1938,6 +1982,7 @@ int tic_image_to_patches_device(tic_handle* h, const uint8_t* d_img, int H, int 
   if (((uintptr_t)d_patches & 3) != 0) return fail(TIC_EINVAL, "d_patches must be 4-byte aligned");
   HIP_TRY(hipSetDevice(h->device));
   const int hn = (H + P - 1) / P, wn = (W + P - 1) / P;
+  touch(h);
   tic::launch_tile_reflect(d_img, H, W, P, hn, wn, d_patches, h->num_cus, h->stream);
   return check_launch();
 }
@@ -1946,6 +1991,7 @@ int tic_patches_to_image_device(tic_handle* h, const float* d_patches, int H, in
   if (!h) return fail(TIC_EINVAL, "null handle");
   if (H <= 0 || W <= 0 || P <= 0 || !d_img || !d_patches) return fail(TIC_EINVAL, "bad arguments");
   HIP_TRY(hipSetDevice(h->device));
+  touch(h);
   tic::launch_stitch(d_patches, H, W, P, (W + P - 1) / P, d_img, h->num_cus, h->stream);
   return check_launch();
 }
@@ -1966,10 +2012,12 @@ int tic_rmbe_image_device(tic_handle* h, float* d_img, int H, int W) {
     rc = ensure(&h->win_in, &h->win_in_bytes, bytes);
     if (!rc) rc = ensure(&h->win_out, &h->win_out_bytes, bytes);
     if (rc) return rc;
+    touch(h);
     tic::launch_window_copy(d_img, W, ps.r0, ps.c0, S, ps.hn, ps.wn, (float*)h->win_in, true, h->num_cus, h->stream);
     if ((rc = check_launch())) return rc;
     rc = rmbe_dev(h, (const float*)h->win_in, n, (float*)h->win_out, Prof{nullptr});
     if (rc) return rc;
+    touch(h);
     tic::launch_window_copy(d_img, W, ps.r0, ps.c0, S, ps.hn, ps.wn, (float*)h->win_out, false, h->num_cus,
                             h->stream);
     if ((rc = check_launch())) return rc;
@@ -1982,6 +2030,7 @@ int tic_round_u8_device(tic_handle* h, const float* d_in, size_t n, uint8_t* d_o
   if (n == 0) return TIC_OK;
   if (!d_in || !d_out) return fail(TIC_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
+  touch(h);
   tic::launch_round_u8(d_in, n, d_out, h->num_cus, h->stream);
   return check_launch();
 }
@@ -1994,6 +2043,7 @@ int tic_histogram_device(tic_handle* h, const uint8_t* d_sym, size_t n, int Q, u
   if (((uintptr_t)d_sym & 3) != 0 || ((uintptr_t)d_counts & 7) != 0)
     return fail(TIC_EINVAL, "d_sym must be 4-byte and d_counts 8-byte aligned");
   HIP_TRY(hipSetDevice(h->device));
+  touch(h);
   tic::launch_histogram(d_sym, n, Q, reinterpret_cast<unsigned long long*>(d_counts), h->num_cus, h->stream);
   return check_launch();
 }
@@ -2005,6 +2055,7 @@ int tic_sse_u8_device(tic_handle* h, const uint8_t* d_a, const uint8_t* d_b, siz
   if (((uintptr_t)d_a & 3) != 0 || ((uintptr_t)d_b & 3) != 0 || ((uintptr_t)d_acc & 7) != 0)
     return fail(TIC_EINVAL, "d_a / d_b must be 4-byte and d_acc 8-byte aligned");
   HIP_TRY(hipSetDevice(h->device));
+  touch(h);
   tic::launch_sse_u8(d_a, d_b, n, reinterpret_cast<unsigned long long*>(d_acc), h->num_cus, h->stream);
   return check_launch();
 }
@@ -2012,6 +2063,7 @@ int tic_sse_u8_device(tic_handle* h, const uint8_t* d_a, const uint8_t* d_b, siz
 int tic_memset_device(tic_handle* h, void* d_ptr, int value, size_t bytes) {
   if (!h || (!d_ptr && bytes)) return fail(TIC_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
+  touch(h);
   HIP_TRY(hipMemsetAsync(d_ptr, value, bytes, h->stream));
   return TIC_OK;
 }
@@ -2024,6 +2076,7 @@ int tic_stream_wait(tic_handle* waiter, tic_handle* signaler) {
   if (!signaler->ev_dep) HIP_TRY(hipEventCreateWithFlags(&signaler->ev_dep, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(signaler->ev_dep, signaler->stream));
   HIP_TRY(hipStreamWaitEvent(waiter->stream, signaler->ev_dep, 0));
+  touch(waiter);
   return TIC_OK;
 }
 
@@ -2044,6 +2097,7 @@ int tic_stream_wait_event(tic_handle* waiter, tic_handle* signaler, int slot) {
   if (!signaler->ev_slot_set[slot]) return TIC_OK;
   HIP_TRY(hipSetDevice(waiter->device));
   HIP_TRY(hipStreamWaitEvent(waiter->stream, signaler->ev_slot[slot], 0));
+  touch(waiter);
   return TIC_OK;
 }
 

@@ -218,6 +218,9 @@ class RcclComm:
         self.comm = C.c_void_p()
         self._ok(self.nccl.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
         self.stream = codec.stream_ptr()
+        # every collective below is followed by a synchronisation, so nothing of ours stays
+        # pending on the codec's stream: its lanes need not fork from it at every call
+        codec.stream_external(False)
         self.d_send = codec.alloc(8 * 6)
         self.d_recv = codec.alloc(8 * 6 * world)
 
