@@ -34,8 +34,8 @@ WINO_FRAC = 16.0 / 36.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--patch", type=int, default=256)

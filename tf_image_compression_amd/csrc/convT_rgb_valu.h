@@ -32,18 +32,18 @@ namespace tic {
 // acc[phase][co] += the 9 (phase, offset) products of one input position.  `self` points at
 // the position in an LDS tile of pitch PS floats per position and LC positions per row, so
 // that offset (-1, 0) is self - LC*PS and (0, -1) is self - PS.  `w` is [3][3][3][CIN].
-template <int CIN, int PS, int LC>
-__device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, float (&acc)[4][3]) {
+// rgb_out_fma_g: the same with chunk c4 of offset (dy, dx) loaded by ld(dy, dx, c4).
+template <int CIN, class Ld>
+__device__ __forceinline__ void rgb_out_fma_g(Ld ld, const float* __restrict__ w, float (&acc)[4][3]) {
   constexpr int C4 = CIN / 4;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
   for (int off = 0; off < 4; ++off) {
     const int dy = -(off >> 1), dx = -(off & 1);
-    const float* src = self + (dy * LC + dx) * PS;
     float x[CIN];
 #pragma unroll
     for (int c4 = 0; c4 < C4; ++c4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * c4);
+      const f32x4 v = ld(dy, dx, c4);
       x[4 * c4] = v.x;
       x[4 * c4 + 1] = v.y;
       x[4 * c4 + 2] = v.z;
@@ -86,6 +86,13 @@ __device__ __forceinline__ void rgb_out_fma(const float* self, const float* __re
       }
     }
   }
+}
+
+template <int CIN, int PS, int LC>
+__device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, float (&acc)[4][3]) {
+  rgb_out_fma_g<CIN>(
+      [&](int dy, int dx, int c4) { return *reinterpret_cast<const f32x4*>(self + (dy * LC + dx) * PS + 4 * c4); }, w,
+      acc);
 }
 
 // + bias, * std + mean, clip -> LDS output tile row-major [.][OW] f32 at output pixel

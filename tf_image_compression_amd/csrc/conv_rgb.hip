@@ -121,32 +121,43 @@ bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int vari
   return false;
 }
 
+template <int C1, int C0, int TA, bool CMP>
+static void dec10_t(const Dec10Args& a, int n, hipStream_t s, int v) {
+  const dim3 grid((a.W + 15) / 16, (a.H + TA - 1) / TA, n), block(64 * TA);
+  switch (v & 3) {
+    case 0: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 0, TA, CMP>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2, 0, TA, CMP>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5, 0, TA, CMP>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5, 0, TA, CMP>), grid, block, 0, s, a); break;
+  }
+}
+
 template <int C1, int C0>
 static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
-  dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n), grid8((a.W + 15) / 16, (a.H + 7) / 8, n);
-  switch (variant) {
-    case 0: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2>), grid, dim3(256), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5>), grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 0, 8>), grid8, dim3(512), 0, s, a); break;
-    case 5: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2, 0, 8>), grid8, dim3(512), 0, s, a); break;
-    case 6: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5, 0, 8>), grid8, dim3(512), 0, s, a); break;
-    case 7: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5, 0, 8>), grid8, dim3(512), 0, s, a); break;
+  const dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n);
+  switch (variant >> 2) {
+    case 0: dec10_t<C1, C0, 4, false>(a, n, s, variant); break;
+    case 1: dec10_t<C1, C0, 8, false>(a, n, s, variant); break;
+    case 2: dec10_t<C1, C0, 4, true>(a, n, s, variant); break;
+    case 3: dec10_t<C1, C0, 8, true>(a, n, s, variant); break;
     // timing probes (TIC_DEC10_VARIANT only; results invalid): decode_1 on the VALU / no decode_0
-    case 8: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1>), grid, dim3(256), 0, s, a); break;
-    case 9: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2>), grid, dim3(256), 0, s, a); break;
+    case 4:
+      if (variant == 16) hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1>), grid, dim3(256), 0, s, a);
+      else if (variant == 17) hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2>), grid, dim3(256), 0, s, a);
+      else return false;
+      break;
     default: return false;
   }
   return true;
 }
 
-// decode_0 weights: scalar loads (even) or LDS (odd); decode_1 weight prefetch 2 or 5
-// steps ahead; tiles of 4 (0-3) or 8 (4-7) decode_1 input rows — all bit-identical
-int dec10_variants() { return 8; }
+// variant bits: 0 decode_0 weights by scalar loads / in LDS; 1 decode_1 weight prefetch 2 / 5
+// steps ahead; 2 tiles of 4 / 8 decode_1 input rows; 3 the padded / compact LDS form — all
+// bit-identical
+int dec10_variants() { return 16; }
 
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {
-  if (variant < 0 || (variant >= dec10_variants() && variant != 8 && variant != 9)) return false;
+  if (variant < 0 || (variant >= dec10_variants() && variant != 16 && variant != 17)) return false;
   if (c1 == 32 && c0 == 32) return dec10_c<32, 32>(a, n, s, variant);
   if (c1 == 32 && c0 == 16) return dec10_c<32, 16>(a, n, s, variant);
   if (c1 == 64 && c0 == 32) return dec10_c<64, 32>(a, n, s, variant);

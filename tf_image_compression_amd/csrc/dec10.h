@@ -28,8 +28,13 @@ namespace tic {
 // addresses from memory (scalar loads), as the two convT_rgb_valu kernels do.  PF: how many
 // K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles).  PROBE:
 // timing experiments only (1 = decode_1 on the VALU, 2 = no decode_0 work; results invalid).
-// None of WSH / PF changes results.
-template <int C1, int C0, bool WSH, int PF, int PROBE, int TA_ = 4>
+// CMP: the compact LDS form — decode_0's input tile unpadded (C0 floats per position, its
+// 16-byte chunks XOR-swizzled per position so the ds_read_b128 of 16 consecutive positions
+// still hits 16 distinct bank slots) with decode_1's input tile aliased into it (a barrier
+// between decode_1's last read of it and the first write of its outputs): 38 KB instead of
+// 56 KB at TA = 4, four workgroups per CU instead of two.
+// None of WSH / PF / TA / CMP changes results.
+template <int C1, int C0, bool WSH, int PF, int PROBE, int TA_ = 4, bool CMP = false>
 struct Dec10 {
   static constexpr int TA = TA_;                    // decode_1 input rows (x 16 columns), one per wave
   static constexpr int NT = 64 * TA;                // threads: one decode_0 input position each
@@ -37,16 +42,24 @@ struct Dec10 {
   static constexpr int LRX = TA + 1, LCX = 17;
   static constexpr int XT = LRX * LCX * PSX;        // decode_1 input tile (floats)
   static constexpr int TH = 2 * TA, TW = 32;        // decode_0 input positions
-  static constexpr int PSY = C0 + 4, LRY = TH + 1, LCY = TW + 1;
+  static constexpr int PSY = CMP ? C0 : C0 + 4, LRY = TH + 1, LCY = TW + 1;
+  static constexpr int NCH = C0 / 4, GRP = 16 / NCH;  // CMP: chunks per position, positions per 256 B
   static constexpr int YT = LRY * LCY * PSY;        // decode_0 input tile incl. halo (floats)
   static constexpr int OT = 2 * TH * 2 * TW * 3;    // decode_0 output staging (floats)
   static constexpr int NB = C0 / 16;
   static constexpr int NSTEP = 9 * KC;
   static constexpr int NSTAGE = LRX * LCX * C4;
   static constexpr int NIT = (NSTAGE + NT - 1) / NT;
-  static constexpr int SMEM = XT + YT + (WSH ? 27 * C0 : 4);
-  static constexpr bool OUT_IN_XT = OT <= XT;       // output staging: the dead input tile, else yt
-  static_assert(OT <= YT && C1 % 16 == 0 && C0 % 16 == 0, "tile");
+  static constexpr int XYT = CMP ? (XT > YT ? XT : YT) : XT + YT;  // xt (+) yt
+  static constexpr int SMEM = XYT + (WSH ? 27 * C0 : 4);
+  static constexpr bool OUT_IN_XT = !CMP && OT <= XT;  // output staging: the dead input tile, else yt
+  static_assert(OT <= YT && C1 % 16 == 0 && C0 % 16 == 0 && NCH <= 16, "tile");
+
+  // float offset of channel chunk c4 of decode_0 input position pos in yt
+  __device__ static int ychunk(int pos, int c4) {
+    if constexpr (CMP) return pos * PSY + 4 * (c4 ^ ((pos / GRP) % NCH));
+    else return pos * PSY + 4 * c4;
+  }
 
   __device__ static f32x4 wglob(const Dec10Args& a, int s, int nb, int li, int lg) {
     const int tap = s / KC, kc = s % KC;
@@ -124,28 +137,32 @@ struct Dec10 {
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) av[p][nb] = wglob(a, p, nb, li, lg);
     }
+    auto put_interior = [&]() {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int py = p >> 1, px = p & 1;
+      for (int p = 0; p < 4; ++p) {
+        const int py = p >> 1, px = p & 1;
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const int co = nb * 16 + lg * 4;
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
-        f32x4 v = acc[p][nb];
-        v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
-        v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
-        v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
-        v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
-        *reinterpret_cast<f32x4*>(&yt[((1 + 2 * wave + py) * LCY + 1 + 2 * li + px) * PSY + co]) = v;
+        for (int nb = 0; nb < NB; ++nb) {
+          const int co = nb * 16 + lg * 4;
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
+          f32x4 v = acc[p][nb];
+          v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
+          v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
+          v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
+          v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
+          *reinterpret_cast<f32x4*>(&yt[ychunk((1 + 2 * wave + py) * LCY + 1 + 2 * li + px, co / 4)]) = v;
+        }
       }
-    }
+    };
+    if constexpr (!CMP) put_interior();
 
     // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
     //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
     //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
     //         q0-1, rows m0-1 .. m0+TA-1: taps 1, 4, 7; lane j = input row m0-1+j, j <= TA) ----
+    const bool row = wave == 0;
+    f32x4 hacc[2][NB];  // [0]: phase 2 (row) / phase 1 (column); [1]: phase 3
     if (wave < 2) {
-      const bool row = wave == 0;
       f32x4 ha[3 * KC][NB];
 #pragma unroll
       for (int ti = 0; ti < 3; ++ti)
@@ -154,7 +171,6 @@ struct Dec10 {
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             ha[ti * KC + kc][nb] = wglob(a, ((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb, li, lg);
-      f32x4 hacc[2][NB];  // [0]: phase 2 (row) / phase 1 (column); [1]: phase 3
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -175,6 +191,12 @@ struct Dec10 {
             for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
         }
       }
+    }
+    if constexpr (CMP) {  // xt lives inside yt: every read of it precedes the first write
+      __syncthreads();
+      put_interior();
+    }
+    if (wave < 2) {
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -195,7 +217,7 @@ struct Dec10 {
           v.y = inside ? fmaxf(__fadd_rn(v.y, bb.y), 0.f) : 0.f;
           v.z = inside ? fmaxf(__fadd_rn(v.z, bb.z), 0.f) : 0.f;
           v.w = inside ? fmaxf(__fadd_rn(v.w, bb.w), 0.f) : 0.f;
-          *reinterpret_cast<f32x4*>(&yt[(ry * LCY + cy) * PSY + co]) = v;
+          *reinterpret_cast<f32x4*>(&yt[ychunk(ry * LCY + cy, co / 4)]) = v;
         }
     }
     __syncthreads();
@@ -205,7 +227,12 @@ struct Dec10 {
     const int r = tid / TW, c = tid % TW;
     float acc3[4][3] = {};
     if constexpr (PROBE == 2) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
-    else rgb_out_fma<C0, PSY, LCY>(&yt[((r + 1) * LCY + (c + 1)) * PSY], WSH ? wsh : a.rgb.wraw, acc3);
+    else
+      rgb_out_fma_g<C0>(
+          [&](int dy, int dx, int c4) {
+            return *reinterpret_cast<const f32x4*>(&yt[ychunk((r + 1 + dy) * LCY + c + 1 + dx, c4)]);
+          },
+          WSH ? wsh : a.rgb.wraw, acc3);
     float* const ot = OUT_IN_XT ? xt : yt;
     if constexpr (!OUT_IN_XT) __syncthreads();
     rgb_out_epilogue(a.rgb, acc3, ot, 2 * TW * 3, r, c);
@@ -217,13 +244,14 @@ struct Dec10 {
 // One workgroup per tile of TA x 16 decode_1 input positions (TA waves): TA = 4 runs two
 // workgroups per CU, TA = 8 one of twice the size (half the halo re-read and per-tile
 // overhead per position).
-template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0, int TA = 4>
-__global__ void __launch_bounds__(64 * TA, 8 / TA) dec10_kernel(const Dec10Args a) {
-  using D = Dec10<C1, C0, WSH, PF, PROBE, TA>;
+template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0, int TA = 4, bool CMP = false>
+__global__ void __launch_bounds__(64 * TA, CMP ? (TA == 4 ? (WSH ? 3 : 4) : 2) : 8 / TA)
+    dec10_kernel(const Dec10Args a) {
+  using D = Dec10<C1, C0, WSH, PF, PROBE, TA, CMP>;
   __shared__ __attribute__((aligned(16))) float smem[D::SMEM];
   float* const xt = smem;
-  float* const yt = smem + D::XT;
-  float* const wsh = smem + D::XT + D::YT;
+  float* const yt = CMP ? smem : smem + D::XT;
+  float* const wsh = smem + D::XYT;
   const int tid = threadIdx.x;
   const int q0 = blockIdx.x * 16, m0 = blockIdx.y * D::TA, nimg = blockIdx.z;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;

@@ -109,6 +109,7 @@ bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int vari
 // decode_1 (C1 -> C0) + decode_0 fused; false if (C1, C0) is not compiled.  Variants are
 // bit-identical (decode_0's weights via scalar loads or LDS).
 int dec10_variants();
+constexpr int kDec10Default = 8;  // compact LDS form, 4 rows, decode_0 weights by scalar loads
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant);
 
 // A chain of stride-1 64->64 layers in one launch (wino_chain.h, conv_chain.hip): args in

@@ -703,7 +703,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         a.rgb.std[c] = h->std[c];
       }
       auto it = lay.tuned_var.find(n);  // fused-tail variants keyed by n on layer L-2
-      int var = it != lay.tuned_var.end() ? it->second : 0;
+      int var = it != lay.tuned_var.end() ? it->second : tic::kDec10Default;
       if (const char* t = getenv("TIC_DEC10_VARIANT")) var = atoi(t);
       else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
         int rc = time_variants(st, tic::dec10_variants(), h->tune_reps,
@@ -1595,12 +1595,6 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   HIP_TRY(ev0.create());
   HIP_TRY(ev1.create());
   hipEvent_t t0 = ev0.e, t1 = ev1.e;
-  struct ForceFork {  // events on h->stream bracket whole steps only if every call forks
-    tic_handle* h;
-    bool was;
-    ~ForceFork() { h->force_fork = was; }
-  } ff{h, h->force_fork};
-  h->force_fork = true;
   auto step = [&]() {
     return h->rmbe() ? rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr})
                      : codec_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, (uint8_t*)d_out);
@@ -1611,6 +1605,9 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     if (r) return r;
     for (int k = 0; k < 3; ++k) {
       HIP_TRY(hipEventRecord(t0, h->stream));
+      // the first step forks from t0; the rest run decoupled, as a caller's steady state
+      // does (t1 follows every lane's join)
+      touch(h);
       for (int q = 0; q < reps; ++q) {
         r = step();
         if (r) return r;
@@ -1661,8 +1658,29 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       const LayerDef& d = l.def;
       const bool first = i == 0, last = i == L - 1;
       if ((first || i == 1) && fuses01(h)) continue;
-      if (i >= L - 2 && fuses_tail(h)) continue;
+      if (i == L - 1 && fuses_tail(h)) continue;
       if (in_chain(h, i)) continue;
+      if (i == L - 2 && fuses_tail(h)) {  // dec10_kernel's variants, keyed by n on this layer
+        if (getenv("TIC_DEC10_VARIANT")) continue;
+        auto iv = l.tuned_var.find(sizes[0]);
+        const int keep = iv != l.tuned_var.end() ? iv->second : tic::kDec10Default;
+        int best_v = keep;
+        float best = cur;
+        for (int v = 0; v < tic::dec10_variants() && !rc; ++v) {
+          if (v == keep) continue;
+          for (int m : sizes) l.tuned_var[m] = v;
+          float ms = 0.f;
+          rc = measure(&ms);
+          if (log) fprintf(stderr, "tune-step dec10 variant %d : %.2f us\n", v, 1e3f * ms);
+          if (!rc && ms < best) {
+            best = ms;
+            best_v = v;
+          }
+        }
+        for (int m : sizes) l.tuned_var[m] = best_v;
+        cur = best;
+        continue;
+      }
       if (first || last) {
         const RgbOutForm fm = first ? RgbOutForm{0, tic::rgb_in_variants()} : rgb_out_form();
         const int keep = first ? l.tuned_var[sizes[0]] : rgb_out_variant(l.tuned_var, sizes[0]);
@@ -1766,10 +1784,10 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   } else if (fuses_tail(h) && i >= L - 2) {
     if (i == L - 2) {
       auto iv = l.tuned_var.find(n);
-      int v = iv != l.tuned_var.end() ? iv->second : 0;
+      int v = iv != l.tuned_var.end() ? iv->second : tic::kDec10Default;
       if (const char* t = getenv("TIC_DEC10_VARIANT")) v = atoi(t);
-      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s,%d,0,%d>", d.cin, d.cout, tf[v & 1], (v & 2) ? 5 : 2,
-               (v & 4) ? 8 : 4);
+      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s,%d,0,%d,%s>", d.cin, d.cout, tf[v & 1], (v & 2) ? 5 : 2,
+               (v & 4) ? 8 : 4, tf[(v >> 3) & 1]);
     }
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name

@@ -1,6 +1,6 @@
 """Where does dec10_kernel's time go?  HIP-event timing of the fused decoder tail of
 model_0 (256x256, 32 patches per launch) per variant, including two timing probes whose
-results are invalid (8: decode_1 on the VALU instead of MFMA, 9: no decode_0 VALU work)."""
+results are invalid (16: decode_1 on the VALU instead of MFMA, 17: no decode_0 VALU work)."""
 import json
 import os
 import subprocess
@@ -31,6 +31,6 @@ if __name__ == "__main__":
         child(int(sys.argv[1]), int(sys.argv[2]))
     else:
         for n in (32, 64):
-            for v in (0, 2, 4, 5, 6, 7):
+            for v in (0, 1, 2, 4, 8, 9, 10, 11, 12, 13, 16, 17):
                 env = dict(os.environ, TIC_DEC10_VARIANT=str(v))
                 subprocess.run([sys.executable, __file__, str(v), str(n)], env=env, check=True, timeout=120)

@@ -1,0 +1,9 @@
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r02o}
+cd $R
+mkdir -p gpurun_out
+source tools/gpu_steps.sh
+step tail_$TAG 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_chain.py
+step bench_$TAG 300 env TIC_TUNE_LOG=1 python bench.py --tune-cache none --no-cpu-baseline
+step bench2_$TAG 300 python bench.py --tune-cache none --no-cpu-baseline
+step bench3_$TAG 300 env TIC_TUNE_LOG=1 python bench.py --model 3 --tune-cache none --no-cpu-baseline
