@@ -259,19 +259,28 @@ def test_autotuned_equals_default(lib_codec):
         b.free()
 
 
-@pytest.mark.parametrize("model_id,P", [(0, 256), (1, 64), (3, 128), (2, 64)])
-def test_fused_first_layers_bit_identical(lib_codec, model_id, P):
-    """enc01_kernel (layers 0+1 through LDS) == the two separate kernels, bit for bit."""
+ENC01_VARIANTS = range(5)  # conv_rgb.hip enc01_variants(): TH1 2/4 padded, 2/4/8 compact
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 256), (0, 48), (1, 64), (3, 128), (2, 64)])
+def test_fused_first_layers_bit_identical(lib_codec, monkeypatch, model_id, P):
+    """enc01_kernel (layers 0+1 through LDS), every variant == the two separate kernels, bit
+    for bit (P = 48: partial edge tiles)."""
     codec, params = lib_codec(model_id, P)
     x = structured_patches(5, P, seed=50 + model_id)
-    codec.set_option("fuse01", 0)
-    idx0, pre0 = codec.encode(x, return_preact=True)
-    codec.set_option("fuse01", 1)
-    idx1, pre1 = codec.encode(x, return_preact=True)
-    assert np.array_equal(pre0, pre1) and np.array_equal(idx0, idx1)
+    try:
+        codec.set_option("fuse01", 0)
+        idx0, pre0 = codec.encode(x, return_preact=True)
+        codec.set_option("fuse01", 1)
+        for v in ENC01_VARIANTS:
+            monkeypatch.setenv("TIC_ENC01_VARIANT", str(v))
+            idx1, pre1 = codec.encode(x, return_preact=True)
+            assert np.array_equal(pre0, pre1) and np.array_equal(idx0, idx1), v
+    finally:
+        codec.set_option("fuse01", 0)
 
 
-def test_fused_rmbe_first_layers_bit_identical():
+def test_fused_rmbe_first_layers_bit_identical(monkeypatch):
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
     from tf_image_compression_amd.topology import RMBE_ID
@@ -281,8 +290,9 @@ def test_fused_rmbe_first_layers_bit_identical():
         c.set_option("fuse01", 0)
         a = c.rmbe_windows(win)
         c.set_option("fuse01", 1)
-        b = c.rmbe_windows(win)
-    assert np.array_equal(a, b)
+        for v in ENC01_VARIANTS:
+            monkeypatch.setenv("TIC_ENC01_VARIANT", str(v))
+            assert np.array_equal(a, c.rmbe_windows(win)), v
 
 
 def test_quan_scale_256(lib_codec):

@@ -650,14 +650,20 @@ __global__ void __launch_bounds__(256) convT_rgb_scatter_kernel(const RgbOutArgs
 // column-deinterleaved LDS tile, zero outside the layer-0 image (layer 1's SAME pad) —
 // then runs layer 1 (stride-2 implicit GEMM, weights from L2 with register prefetch).
 // The full-resolution C0-channel layer-0 activation never reaches HBM.
+// CMP: the compact LDS form — layer 0's results are held in registers until every wave has
+// finished reading the RGB planes, then written into the layer-1 tile that aliases them;
+// that tile is unpadded (C0 floats per slot) with its 16-byte chunks XOR-swizzled per slot
+// (16 consecutive slots -> 16 distinct bank slots for ds_read_b128): 39 KB instead of 64 KB
+// at TH1 = 4, four workgroups per CU instead of two.  Bit-identical to the padded form.
 // ---------------------------------------------------------------------------------------
-template <int C0, int C1, int TH1, bool U8>
-__global__ void __launch_bounds__(256) enc01_kernel(const Enc01Args a) {
+template <int C0, int C1, int TH1, bool U8, bool CMP = false>
+__global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kernel(const Enc01Args a) {
   static_assert(C0 % 16 == 0 && C1 % 16 == 0 && (TH1 % 4 == 0 || TH1 == 2), "tile");
   constexpr int R0 = 4 * TH1 + 3;        // RGB rows
   constexpr int QJ = 17;                 // entries per col%4 plane (67 cols -> 17)
   constexpr int RGBP = R0 * 4 * QJ;      // floats per channel plane
-  constexpr int LR1 = 2 * TH1 + 1, LC1 = 34, PS1 = C0 + 8;
+  constexpr int LR1 = 2 * TH1 + 1, LC1 = 34, PS1 = CMP ? C0 : C0 + 8;
+  constexpr int NCH = C0 / 4, GRP = 16 / NCH;  // CMP swizzle: chunks per slot, slots per 256 B
   constexpr int T1 = LR1 * LC1 * PS1;    // layer-1 input tile (floats)
   constexpr int NSLOT = LR1 * LC1;
   constexpr int NBLK0 = (NSLOT + 15) / 16;
@@ -668,9 +674,15 @@ __global__ void __launch_bounds__(256) enc01_kernel(const Enc01Args a) {
   constexpr int MB = TH1 / WR;
   constexpr int NB1 = C1 / 16 / WC;
   static_assert((C1 / 16) % WC == 0, "layer-1 channel split");
-  __shared__ __attribute__((aligned(16))) float smem[T1 + 3 * RGBP];
+  constexpr int SMEM = CMP ? (T1 > 3 * RGBP ? T1 : 3 * RGBP) : T1 + 3 * RGBP;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float* const t1 = smem;
-  float* const rgb = smem + T1;
+  float* const rgb = CMP ? smem : smem + T1;
+  // float offset of channel chunk c4 of layer-1 tile slot `slot`
+  auto t1c = [](int slot, int c4) {
+    if constexpr (CMP) return slot * PS1 + 4 * (c4 ^ ((slot / GRP) % NCH));
+    else return slot * PS1 + 4 * c4;
+  };
 
   const int tid = threadIdx.x;
   const int gx0 = blockIdx.x * 16, gy0 = blockIdx.y * TH1, nimg = blockIdx.z;
@@ -762,7 +774,30 @@ __global__ void __launch_bounds__(256) enc01_kernel(const Enc01Args a) {
         dl[pl][t] = k < 27 ? c * RGBP + ky * 4 * QJ + (q & 3) * QJ + (q >> 2) : -1;
       }
     }
-    for (int blk = wave; blk < NBLK0; blk += 4) {
+    constexpr int NPW = (NBLK0 + 3) / 4;  // blocks per wave
+    f32x4 res[CMP ? NPW : 1][NB0];         // CMP: layer-0 results held until the RGB planes are dead
+    auto put0 = [&](int slot, bool valid, const f32x4 (&acc)[NB0]) {
+#pragma unroll
+      for (int nb = 0; nb < NB0; ++nb) {
+        f32x4 v = acc[nb];
+        v.x = valid ? fmaxf(__fadd_rn(v.x, bb[nb].x), 0.f) : 0.f;
+        v.y = valid ? fmaxf(__fadd_rn(v.y, bb[nb].y), 0.f) : 0.f;
+        v.z = valid ? fmaxf(__fadd_rn(v.z, bb[nb].z), 0.f) : 0.f;
+        v.w = valid ? fmaxf(__fadd_rn(v.w, bb[nb].w), 0.f) : 0.f;
+        *reinterpret_cast<f32x4*>(&t1[t1c(slot, nb * 4 + lg)]) = v;
+      }
+    };
+    auto slot_valid = [&](int slot) {
+      const int r = slot / LC1, cs = slot % LC1;
+      const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
+      const int exl = 2 * j + plane;
+      const int ey = ey0 + r, ex = ex0 + exl;
+      return slot < NSLOT && exl < 33 && ey >= 0 && ey < a.H1 && ex >= 0 && ex < a.W1;
+    };
+#pragma unroll
+    for (int jb = 0; jb < NPW; ++jb) {
+      const int blk = wave + 4 * jb;
+      if (blk >= NBLK0) break;
       const int slot = blk * 16 + li;
       const int r = slot / LC1, cs = slot % LC1;
       const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
@@ -784,18 +819,19 @@ __global__ void __launch_bounds__(256) enc01_kernel(const Enc01Args a) {
 #pragma unroll
         for (int nb = 0; nb < NB0; ++nb) acc[nb] = mfma4(t < 4 ? w0[nb][t & 3] : w1[nb][t & 3], b[t], acc[nb]);
       // lane holds channels nb*16 + 4 lg .. +3 of slot; relu; zero outside layer 0's image
-      const int ey = ey0 + r, ex = ex0 + exl;
-      const bool valid = rd && ey >= 0 && ey < a.H1 && ex >= 0 && ex < a.W1;
-      if (slot < NSLOT) {
+      if constexpr (CMP) {
 #pragma unroll
-        for (int nb = 0; nb < NB0; ++nb) {
-          f32x4 v = acc[nb];
-          v.x = valid ? fmaxf(__fadd_rn(v.x, bb[nb].x), 0.f) : 0.f;
-          v.y = valid ? fmaxf(__fadd_rn(v.y, bb[nb].y), 0.f) : 0.f;
-          v.z = valid ? fmaxf(__fadd_rn(v.z, bb[nb].z), 0.f) : 0.f;
-          v.w = valid ? fmaxf(__fadd_rn(v.w, bb[nb].w), 0.f) : 0.f;
-          *reinterpret_cast<f32x4*>(&t1[slot * PS1 + nb * 16 + lg * 4]) = v;
-        }
+        for (int nb = 0; nb < NB0; ++nb) res[jb][nb] = acc[nb];
+      } else if (slot < NSLOT) {
+        put0(slot, slot_valid(slot), acc);
+      }
+    }
+    if constexpr (CMP) {
+      __syncthreads();  // every wave is done with the RGB planes the tile overwrites
+#pragma unroll
+      for (int jb = 0; jb < NPW; ++jb) {
+        const int blk = wave + 4 * jb, slot = blk * 16 + li;
+        if (blk < NBLK0 && slot < NSLOT) put0(slot, slot_valid(slot), res[jb]);
       }
     }
   }
@@ -813,7 +849,7 @@ __global__ void __launch_bounds__(256) enc01_kernel(const Enc01Args a) {
     for (int mb = 0; mb < MB; ++mb) {
       const int r = wr * MB + mb;
       const int lp = (2 * r + ky) * LC1 + (kx & 1) * 17 + li + (kx >> 1);
-      dst[mb] = *reinterpret_cast<const f32x4*>(&t1[lp * PS1 + kc * 16 + lg * 4]);
+      dst[mb] = *reinterpret_cast<const f32x4*>(&t1[t1c(lp, kc * 4 + lg)]);
     }
   };
   f32x4 bq[2][MB];

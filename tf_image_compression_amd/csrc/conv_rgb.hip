@@ -41,22 +41,28 @@ bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream
 // (TH 4/8/16), 6-11 VALU form (TW 64/32/16; 9-11 persistent, software-pipelined).  The form is a fixed policy (default VALU;
 // TIC_RGB_OUT_FORM=dense|scatter for experiments); tuning picks a tiling within the form,
 // so it never changes results.
-int enc01_variants() { return 2; }  // TH1 = 2, 4
+// TH1 = 2, 4 (padded LDS form), 2, 4, 8 (compact form) — all bit-identical
+int enc01_variants() { return 5; }
 
-template <int C0, int C1, int TH1>
+template <int C0, int C1, int TH1, bool CMP>
 static bool enc01_th(bool u8_input, const Enc01Args& a, int n, hipStream_t s) {
   dim3 grid((a.W2 + 15) / 16, (a.H2 + TH1 - 1) / TH1, n);
   if (u8_input)
-    hipLaunchKernelGGL((enc01_kernel<C0, C1, TH1, true>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((enc01_kernel<C0, C1, TH1, true, CMP>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((enc01_kernel<C0, C1, TH1, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((enc01_kernel<C0, C1, TH1, false, CMP>), grid, dim3(256), 0, s, a);
   return true;
 }
 
 template <int C0, int C1>
 static bool enc01_c(bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant) {
-  if (variant == 0) return enc01_th<C0, C1, 2>(u8_input, a, n, s);
-  if (variant == 1) return enc01_th<C0, C1, 4>(u8_input, a, n, s);
+  switch (variant) {
+    case 0: return enc01_th<C0, C1, 2, false>(u8_input, a, n, s);
+    case 1: return enc01_th<C0, C1, 4, false>(u8_input, a, n, s);
+    case 2: return enc01_th<C0, C1, 2, true>(u8_input, a, n, s);
+    case 3: return enc01_th<C0, C1, 4, true>(u8_input, a, n, s);
+    case 4: return enc01_th<C0, C1, 8, true>(u8_input, a, n, s);
+  }
   return false;
 }
 

@@ -102,6 +102,7 @@ const ConvEntry* conv_registry_t2(int* count);
 // bit-identical.
 int rgb_in_variants();
 int enc01_variants();
+constexpr int kEnc01Default = 3;  // compact LDS form, 4 layer-1 rows
 bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant);
 int rgb_out_variants();
 bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant);

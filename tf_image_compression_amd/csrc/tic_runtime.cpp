@@ -662,8 +662,9 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         a.std[c] = h->std[c];
       }
       auto it = lay.tuned_var.find(-n);  // fused-pair variants keyed by -n
-      int var = it != lay.tuned_var.end() ? it->second : 1;
-      if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
+      int var = it != lay.tuned_var.end() ? it->second : tic::kEnc01Default;
+      if (const char* t = getenv("TIC_ENC01_VARIANT")) var = atoi(t);
+      else if (h->tune_reps > 0 && it == lay.tuned_var.end()) {
         int rc = time_variants(st, tic::enc01_variants(), h->tune_reps,
                                [&](int v) { return tic::launch_enc01(d.cout, l1r.def.cout, !h->rmbe(), a, n, st, v); },
                                &var, "enc01", n);
@@ -1657,27 +1658,31 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       LayerRT& l = h->layers[i];
       const LayerDef& d = l.def;
       const bool first = i == 0, last = i == L - 1;
-      if ((first || i == 1) && fuses01(h)) continue;
+      if (i == 1 && fuses01(h)) continue;
       if (i == L - 1 && fuses_tail(h)) continue;
       if (in_chain(h, i)) continue;
-      if (i == L - 2 && fuses_tail(h)) {  // dec10_kernel's variants, keyed by n on this layer
-        if (getenv("TIC_DEC10_VARIANT")) continue;
-        auto iv = l.tuned_var.find(sizes[0]);
-        const int keep = iv != l.tuned_var.end() ? iv->second : tic::kDec10Default;
+      // the fused pairs' variants: dec10_kernel keyed by n on layer L-2, enc01_kernel by -n
+      // on layer 0
+      const bool tail = i == L - 2 && fuses_tail(h), pair = first && fuses01(h);
+      if (tail || pair) {
+        if (getenv(tail ? "TIC_DEC10_VARIANT" : "TIC_ENC01_VARIANT")) continue;
+        const int sg = tail ? 1 : -1;
+        auto iv = l.tuned_var.find(sg * sizes[0]);
+        const int keep = iv != l.tuned_var.end() ? iv->second : tail ? tic::kDec10Default : tic::kEnc01Default;
         int best_v = keep;
         float best = cur;
-        for (int v = 0; v < tic::dec10_variants() && !rc; ++v) {
+        for (int v = 0; v < (tail ? tic::dec10_variants() : tic::enc01_variants()) && !rc; ++v) {
           if (v == keep) continue;
-          for (int m : sizes) l.tuned_var[m] = v;
+          for (int m : sizes) l.tuned_var[sg * m] = v;
           float ms = 0.f;
           rc = measure(&ms);
-          if (log) fprintf(stderr, "tune-step dec10 variant %d : %.2f us\n", v, 1e3f * ms);
+          if (log) fprintf(stderr, "tune-step %s variant %d : %.2f us\n", tail ? "dec10" : "enc01", v, 1e3f * ms);
           if (!rc && ms < best) {
             best = ms;
             best_v = v;
           }
         }
-        for (int m : sizes) l.tuned_var[m] = best_v;
+        for (int m : sizes) l.tuned_var[sg * m] = best_v;
         cur = best;
         continue;
       }
@@ -1792,9 +1797,11 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
       auto iv = l.tuned_var.find(-n);
-      const int v = iv != l.tuned_var.end() ? iv->second : 1;
-      snprintf(buf, sizeof buf, "enc01_kernel<%d,%d,%d,%s>", d.cout, h->layers[1].def.cout, v == 0 ? 2 : 4,
-               tf[!h->rmbe()]);
+      int v = iv != l.tuned_var.end() ? iv->second : tic::kEnc01Default;
+      if (const char* t = getenv("TIC_ENC01_VARIANT")) v = atoi(t);
+      static const int th1[5] = {2, 4, 2, 4, 8};
+      snprintf(buf, sizeof buf, "enc01_kernel<%d,%d,%d,%s,%s>", d.cout, h->layers[1].def.cout, th1[v % 5],
+               tf[!h->rmbe()], tf[v >= 2]);
     }
   } else if (i == 0 || i == L - 1) {
     auto iv = l.tuned_var.find(n);
