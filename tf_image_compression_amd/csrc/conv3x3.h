@@ -674,10 +674,15 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   constexpr int MB = TH1 / WR;
   constexpr int NB1 = C1 / 16 / WC;
   static_assert((C1 / 16) % WC == 0, "layer-1 channel split");
-  constexpr int SMEM = CMP ? (T1 > 3 * RGBP ? T1 : 3 * RGBP) : T1 + 3 * RGBP;
+  // u8 input: the 3 x 256 normalised values (x - mean) / std as a table, dead once staged
+  // (CMP: after the RGB planes, inside the region the layer-1 tile later takes over)
+  constexpr int LUT_OFF = CMP ? 3 * RGBP : T1 + 3 * RGBP;
+  constexpr int SMEM0 = CMP ? (T1 > 3 * RGBP ? T1 : 3 * RGBP) : T1 + 3 * RGBP;
+  constexpr int SMEM = U8 && LUT_OFF + 768 > SMEM0 ? LUT_OFF + 768 : SMEM0;
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float* const t1 = smem;
   float* const rgb = CMP ? smem : smem + T1;
+  float* const lut = smem + LUT_OFF;
   // float offset of channel chunk c4 of layer-1 tile slot `slot`
   auto t1c = [](int slot, int c4) {
     if constexpr (CMP) return slot * PS1 + 4 * (c4 ^ ((slot / GRP) % NCH));
@@ -711,24 +716,31 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
     rgb[c * RGBP + (rr * 4 + (col & 3)) * QJ + (col >> 2)] = __fdiv_rn(__fsub_rn(x, a.mean[c]), a.std[c]);
   };
   // zero the planes first where the tile leaves the image (SAME padding)
-  const bool edge = iy0 < 0 || ix0 < 0 || iy0 + R0 > a.H || ix0 + 67 > a.W || !U8 || (ix0 * 3) % 4 != 0;
-  if (edge) {
+  const bool edge = iy0 < 0 || ix0 < 0 || iy0 + R0 > a.H || ix0 + 68 > a.W || !U8 || (ix0 * 3) % 4 != 0;
+  if (edge)
     for (int e = tid; e < 3 * RGBP; e += 256) rgb[e] = 0.f;
-    __syncthreads();
-  }
+  if constexpr (U8)
+    for (int e = tid; e < 768; e += 256)
+      lut[e] = __fdiv_rn(__fsub_rn((float)(e & 255), a.mean[e >> 8]), a.std[e >> 8]);
+  if (edge || U8) __syncthreads();
   if constexpr (U8) {
     if (!edge) {
-      // interior: each thread unpacks 32-bit words of the 201-byte RGB row segments
-      constexpr int WPR = 51;  // 204 bytes >= 67 * 3
-      for (int e = tid; e < R0 * WPR; e += 256) {
-        const int rr = e / WPR, w = e % WPR;
-        const size_t boff = ((size_t)(nimg * a.H + iy0 + rr) * a.W + ix0) * 3 + 4 * w;
-        const uint32_t word = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + boff);
+      // interior: each thread unpacks one 4-pixel group (12 bytes) of a 68-pixel row segment;
+      // pixel k of group g is column 4g + k: plane k, entry g
+      constexpr int GPR = 17;
+      for (int e = tid; e < R0 * GPR; e += 256) {
+        const int rr = e / GPR, g = e % GPR;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(
+            reinterpret_cast<const uint8_t*>(a.in) + ((size_t)(nimg * a.H + iy0 + rr) * a.W + ix0) * 3 + 12 * g);
+        const uint32_t w[3] = {src[0], src[1], src[2]};
+        float* const dst = rgb + rr * 4 * QJ + g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int pb = 4 * w + i;
-          if (pb < 201) put_rgb(rr, pb / 3, pb % 3, (float)((word >> (8 * i)) & 0xff));
-        }
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int b = 3 * k + c;
+            dst[c * RGBP + k * QJ] = lut[c * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xff)];
+          }
       }
     }
   }
@@ -740,10 +752,11 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
         const size_t off = ((size_t)(nimg * a.H + iy) * a.W + ix) * 3;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          float x;
-          if constexpr (U8) x = reinterpret_cast<const uint8_t*>(a.in)[off + c];
-          else x = reinterpret_cast<const float*>(a.in)[off + c];
-          put_rgb(rr, col, c, x);
+          if constexpr (U8)
+            rgb[c * RGBP + (rr * 4 + (col & 3)) * QJ + (col >> 2)] =
+                lut[c * 256 + reinterpret_cast<const uint8_t*>(a.in)[off + c]];
+          else
+            put_rgb(rr, col, c, reinterpret_cast<const float*>(a.in)[off + c]);
         }
       }
     }

@@ -32,8 +32,11 @@ namespace tic {
 // acc[phase][co] += the 9 (phase, offset) products of one input position.  `self` points at
 // the position in an LDS tile of pitch PS floats per position and LC positions per row, so
 // that offset (-1, 0) is self - LC*PS and (0, -1) is self - PS.  `w` is [3][3][3][CIN].
-// rgb_out_fma_g: the same with chunk c4 of offset (dy, dx) loaded by ld(dy, dx, c4).
-template <int CIN, class Ld>
+// rgb_out_fma_g: the same with chunk c4 of offset (dy, dx) loaded by ld(dy, dx, c4); PK
+// selects packed fmas (v_pk_fma_f32, whose two weights must sit in an aligned SGPR pair —
+// s_mov repacking per instruction) or two interleaved plain v_fma_f32 chains (one SGPR
+// operand each; on CDNA4 two v_fma_f32 issue in the time of one v_pk_fma_f32).
+template <int CIN, bool PK = true, class Ld>
 __device__ __forceinline__ void rgb_out_fma_g(Ld ld, const float* __restrict__ w, float (&acc)[4][3]) {
   constexpr int C4 = CIN / 4;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -64,15 +67,26 @@ __device__ __forceinline__ void rgb_out_fma_g(Ld ld, const float* __restrict__ w
       for (int co = 0; co < 3; ++co) {
         const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
         const float* wb = w + ((kyb * 3 + kxb) * 3 + co) * CIN;
-        f32x2 s2 = {acc[pa][co], acc[pb][co]};
+        if constexpr (PK) {
+          f32x2 s2 = {acc[pa][co], acc[pb][co]};
 #pragma unroll
-        for (int ci = 0; ci < CIN; ++ci) {
-          const f32x2 xx = {x[ci], x[ci]};
-          const f32x2 ww = {wa[ci], wb[ci]};
-          s2 = __builtin_elementwise_fma(xx, ww, s2);
+          for (int ci = 0; ci < CIN; ++ci) {
+            const f32x2 xx = {x[ci], x[ci]};
+            const f32x2 ww = {wa[ci], wb[ci]};
+            s2 = __builtin_elementwise_fma(xx, ww, s2);
+          }
+          acc[pa][co] = s2.x;
+          acc[pb][co] = s2.y;
+        } else {
+          float sa = acc[pa][co], sb = acc[pb][co];
+#pragma unroll
+          for (int ci = 0; ci < CIN; ++ci) {
+            sa = fmaf(x[ci], wa[ci], sa);
+            sb = fmaf(x[ci], wb[ci], sb);
+          }
+          acc[pa][co] = sa;
+          acc[pb][co] = sb;
         }
-        acc[pa][co] = s2.x;
-        acc[pb][co] = s2.y;
       }
     }
     if (np & 1) {

@@ -127,14 +127,16 @@ bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int vari
   return false;
 }
 
+// decode_0's weights always by scalar loads here: staging them in LDS (WSH) measured 25-35 %
+// slower in every form (profiles/dec10_probe_r02*.log)
 template <int C1, int C0, int TA, bool CMP>
 static void dec10_t(const Dec10Args& a, int n, hipStream_t s, int v) {
   const dim3 grid((a.W + 15) / 16, (a.H + TA - 1) / TA, n), block(64 * TA);
   switch (v & 3) {
-    case 0: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 0, TA, CMP>), grid, block, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 2, 0, TA, CMP>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5, 0, TA, CMP>), grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL((dec10_kernel<C1, C0, true, 5, 0, TA, CMP>), grid, block, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 0, TA, CMP, true>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 0, TA, CMP, false>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5, 0, TA, CMP, true>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 5, 0, TA, CMP, false>), grid, block, 0, s, a); break;
   }
 }
 
@@ -146,24 +148,29 @@ static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
     case 1: dec10_t<C1, C0, 8, false>(a, n, s, variant); break;
     case 2: dec10_t<C1, C0, 4, true>(a, n, s, variant); break;
     case 3: dec10_t<C1, C0, 8, true>(a, n, s, variant); break;
-    // timing probes (TIC_DEC10_VARIANT only; results invalid): decode_1 on the VALU / no decode_0
+    // timing probes of variant 8 (TIC_DEC10_VARIANT only; results invalid): without decode_1's
+    // MFMAs / decode_0 / the input loads / decode_1's weight loads (dec10.h PROBE)
     case 4:
-      if (variant == 16) hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1>), grid, dim3(256), 0, s, a);
-      else if (variant == 17) hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2>), grid, dim3(256), 0, s, a);
-      else return false;
+      switch (variant) {
+        case 16: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1, 4, true>), grid, dim3(256), 0, s, a); break;
+        case 17: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2, 4, true>), grid, dim3(256), 0, s, a); break;
+        case 18: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 4, 4, true>), grid, dim3(256), 0, s, a); break;
+        case 19: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 8, 4, true>), grid, dim3(256), 0, s, a); break;
+        default: return false;
+      }
       break;
     default: return false;
   }
   return true;
 }
 
-// variant bits: 0 decode_0 weights by scalar loads / in LDS; 1 decode_1 weight prefetch 2 / 5
+// variant bits: 0 decode_0 by packed / plain fmas; 1 decode_1 weight prefetch 2 / 5
 // steps ahead; 2 tiles of 4 / 8 decode_1 input rows; 3 the padded / compact LDS form — all
 // bit-identical
 int dec10_variants() { return 16; }
 
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {
-  if (variant < 0 || (variant >= dec10_variants() && variant != 16 && variant != 17)) return false;
+  if (variant < 0 || variant >= 20) return false;
   if (c1 == 32 && c0 == 32) return dec10_c<32, 32>(a, n, s, variant);
   if (c1 == 32 && c0 == 16) return dec10_c<32, 16>(a, n, s, variant);
   if (c1 == 64 && c0 == 32) return dec10_c<64, 32>(a, n, s, variant);

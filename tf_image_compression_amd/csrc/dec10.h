@@ -27,14 +27,16 @@ namespace tic {
 // WSH: decode_0's weights staged in LDS (broadcast ds_read_b128) or read with wave-uniform
 // addresses from memory (scalar loads), as the two convT_rgb_valu kernels do.  PF: how many
 // K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles).  PROBE:
-// timing experiments only (1 = decode_1 on the VALU, 2 = no decode_0 work; results invalid).
+// timing experiments only, a mask of work left out (results invalid): 1 decode_1's MFMAs,
+// 2 decode_0, 4 the input tile's loads, 8 decode_1's weight loads.
 // CMP: the compact LDS form — decode_0's input tile unpadded (C0 floats per position, its
 // 16-byte chunks XOR-swizzled per position so the ds_read_b128 of 16 consecutive positions
 // still hits 16 distinct bank slots) with decode_1's input tile aliased into it (a barrier
 // between decode_1's last read of it and the first write of its outputs): 38 KB instead of
 // 56 KB at TA = 4, four workgroups per CU instead of two.
-// None of WSH / PF / TA / CMP changes results.
-template <int C1, int C0, bool WSH, int PF, int PROBE, int TA_ = 4, bool CMP = false>
+// PK: decode_0 by packed or plain fmas (rgb_out_fma_g).
+// None of WSH / PF / TA / CMP / PK changes results.
+template <int C1, int C0, bool WSH, int PF, int PROBE, int TA_ = 4, bool CMP = false, bool PK = true>
 struct Dec10 {
   static constexpr int TA = TA_;                    // decode_1 input rows (x 16 columns), one per wave
   static constexpr int NT = 64 * TA;                // threads: one decode_0 input position each
@@ -76,7 +78,7 @@ struct Dec10 {
       if (e < NSTAGE) {
         const int c4 = e % C4, pe = e / C4, col = pe % LCX, row = pe / LCX;
         const int iy = m0 - 1 + row, ix = q0 - 1 + col;
-        if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+        if (!(PROBE & 4) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
           pre[i] = *reinterpret_cast<const f32x4*>(a.in + ((size_t)(nimg * a.H + iy) * a.W + ix) * C1 + c4 * 4);
       }
     }
@@ -117,7 +119,8 @@ struct Dec10 {
       const int c = s & 1;
       if (s + PF < NSTEP) {
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(a, s + PF, nb, li, lg);
+        for (int nb = 0; nb < NB; ++nb)
+          av[(s + PF) % (PF + 1)][nb] = (PROBE & 8) ? av[s % (PF + 1)][nb] : wglob(a, s + PF, nb, li, lg);
       }
       if (s + 1 < NSTEP) bq[c ^ 1] = load_b(s + 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -126,7 +129,7 @@ struct Dec10 {
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
-          if constexpr (PROBE == 1) acc[ph][nb][t] += av[s % (PF + 1)][nb][t] * bq[c][t];
+          if constexpr (PROBE & 1) acc[ph][nb][t] = fmaxf(acc[ph][nb][t], bq[c][t]);  // keep the reads live
           else acc[ph][nb] = mfma4(av[s % (PF + 1)][nb][t], bq[c][t], acc[ph][nb]);
         }
       __builtin_amdgcn_sched_barrier(0);
@@ -226,9 +229,9 @@ struct Dec10 {
     //         when it is too small, in yt once every thread has read its inputs) ----
     const int r = tid / TW, c = tid % TW;
     float acc3[4][3] = {};
-    if constexpr (PROBE == 2) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
+    if constexpr ((PROBE & 2) != 0) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
     else
-      rgb_out_fma_g<C0>(
+      rgb_out_fma_g<C0, PK>(
           [&](int dy, int dx, int c4) {
             return *reinterpret_cast<const f32x4*>(&yt[ychunk((r + 1 + dy) * LCY + c + 1 + dx, c4)]);
           },
@@ -244,10 +247,10 @@ struct Dec10 {
 // One workgroup per tile of TA x 16 decode_1 input positions (TA waves): TA = 4 runs two
 // workgroups per CU, TA = 8 one of twice the size (half the halo re-read and per-tile
 // overhead per position).
-template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0, int TA = 4, bool CMP = false>
+template <int C1, int C0, bool WSH, int PF = 2, int PROBE = 0, int TA = 4, bool CMP = false, bool PK = true>
 __global__ void __launch_bounds__(64 * TA, CMP ? (TA == 4 ? (WSH ? 3 : 4) : 2) : 8 / TA)
     dec10_kernel(const Dec10Args a) {
-  using D = Dec10<C1, C0, WSH, PF, PROBE, TA, CMP>;
+  using D = Dec10<C1, C0, WSH, PF, PROBE, TA, CMP, PK>;
   __shared__ __attribute__((aligned(16))) float smem[D::SMEM];
   float* const xt = smem;
   float* const yt = CMP ? smem : smem + D::XT;

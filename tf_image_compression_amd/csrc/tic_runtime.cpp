@@ -1791,8 +1791,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
       auto iv = l.tuned_var.find(n);
       int v = iv != l.tuned_var.end() ? iv->second : tic::kDec10Default;
       if (const char* t = getenv("TIC_DEC10_VARIANT")) v = atoi(t);
-      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,%s,%d,0,%d,%s>", d.cin, d.cout, tf[v & 1], (v & 2) ? 5 : 2,
-               (v & 4) ? 8 : 4, tf[(v >> 3) & 1]);
+      snprintf(buf, sizeof buf, "dec10_kernel<%d,%d,false,%d,0,%d,%s,%s>", d.cin, d.cout, (v & 2) ? 5 : 2,
+               (v & 4) ? 8 : 4, tf[(v >> 3) & 1], tf[!(v & 1)]);
     }
   } else if (fuses01(h) && (i == 0 || i == 1)) {
     if (i == 0) {  // layer 1 runs inside layer 0's launch: empty name
