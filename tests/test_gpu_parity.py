@@ -366,10 +366,9 @@ def test_fused_tail_bit_identical(lib_codec, monkeypatch, model_id, P):
         u0, f0 = codec.decode(idx, return_float=True)
         codec.set_option("fuse_tail", 1)
         outs = []
-        for v in range(16):  # conv_rgb.hip dec10_variants(): WSH x PF x TA x CMP
+        for v in range(16):  # conv_rgb.hip dec10_variants(): PK x PF x TA x CMP
             monkeypatch.setenv("TIC_DEC10_VARIANT", str(v))
             outs.append(codec.decode(idx, return_float=True))
-
     finally:
         codec.set_option("fuse_tail", 0)
     for u1, f1 in outs:

@@ -25,6 +25,7 @@
 // within each — the same for every TW and both kernels, so every tiling is bit-identical.
 // The helpers below are shared with the fused decoder tail.
 #pragma once
+#include <type_traits>
 #include "conv3x3.h"
 
 namespace tic {
@@ -35,83 +36,102 @@ namespace tic {
 // rgb_out_fma_g: the same with chunk c4 of offset (dy, dx) loaded by ld(dy, dx, c4); PK
 // selects packed fmas (v_pk_fma_f32, whose two weights must sit in an aligned SGPR pair —
 // s_mov repacking per instruction) or two interleaved plain v_fma_f32 chains (one SGPR
-// operand each; on CDNA4 two v_fma_f32 issue in the time of one v_pk_fma_f32).
-template <int CIN, bool PK = true, class Ld>
-__device__ __forceinline__ void rgb_out_fma_g(Ld ld, const float* __restrict__ w, float (&acc)[4][3]) {
-  constexpr int C4 = CIN / 4;
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
+// operand each).  Weights in global memory (WG) are read through the constant address
+// space: wave-uniform scalar loads even where the kernel also stores to global memory
+// earlier on the path (the persistent forms), which would otherwise make them vector
+// loads; weights staged in LDS (!WG) are read as they are.  Offsets and phases are
+// template constants so every acc index is one before any optimisation runs (computed
+// indices left acc in scratch in some instantiations).
+namespace rgbout {
+typedef const __attribute__((address_space(4))) float* cfp;
+template <bool WG> using wptr = typename std::conditional<WG, cfp, const float*>::type;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// kernel tap (ky or kx) of phase bit p at input offset d (0 or -1): T(0) = {(0,0), (2,-1)}, T(1) = {(1,0)}
+constexpr int tap(int p, int d) { return p ? 1 : (d == 0 ? 0 : 2); }
+// phases using offset OFF (py = 0 when dy = -1, px = 0 when dx = -1): 0 -> 0,1,2,3; 1 -> 0,2;
+// 2 -> 0,1; 3 -> 0
+constexpr int nphase(int off) { return off == 0 ? 4 : off == 3 ? 1 : 2; }
+constexpr int phase(int off, int k) { return off == 1 ? 2 * k : k; }
+
+template <int CIN, int OFF, int PA, class W>
+__device__ __forceinline__ W wrow(W w, int co) {
+  return w + ((tap(PA >> 1, -(OFF >> 1)) * 3 + tap(PA & 1, -(OFF & 1))) * 3 + co) * CIN;
+}
+
+// phases PA and PB (PB < 0: PA alone) of one offset, each output's chain ci ascending
+template <int CIN, bool PK, int OFF, int PA, int PB, class W>
+__device__ __forceinline__ void chains(const float (&x)[CIN], W w, f32x4 (&acc)[4]) {
 #pragma unroll
-  for (int off = 0; off < 4; ++off) {
-    const int dy = -(off >> 1), dx = -(off & 1);
-    float x[CIN];
+  for (int co = 0; co < 3; ++co) {
+    const W wa = wrow<CIN, OFF, PA>(w, co);
+    if constexpr (PB < 0) {
 #pragma unroll
-    for (int c4 = 0; c4 < C4; ++c4) {
-      const f32x4 v = ld(dy, dx, c4);
-      x[4 * c4] = v.x;
-      x[4 * c4 + 1] = v.y;
-      x[4 * c4 + 2] = v.z;
-      x[4 * c4 + 3] = v.w;
-    }
-    // phases using this offset, paired so one packed fma (v_pk_fma_f32) advances two
-    // outputs' chains by one step each — every output's own fma order is unchanged
-    int ph[4], np = 0;
+      for (int ci = 0; ci < CIN; ++ci) acc[PA][co] = fmaf(x[ci], wa[ci], acc[PA][co]);
+    } else {
+      const W wb = wrow<CIN, OFF, PB>(w, co);
+      if constexpr (PK) {
+        f32x2 s2 = {acc[PA][co], acc[PB][co]};
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
-      if (!((dy != 0 && (p >> 1) == 1) || (dx != 0 && (p & 1) == 1))) ph[np++] = p;
-#pragma unroll
-    for (int k = 0; k + 1 < np; k += 2) {
-      const int pa = ph[k], pb = ph[k + 1];
-      const int kya = (pa >> 1) ? 1 : (dy == 0 ? 0 : 2), kxa = (pa & 1) ? 1 : (dx == 0 ? 0 : 2);
-      const int kyb = (pb >> 1) ? 1 : (dy == 0 ? 0 : 2), kxb = (pb & 1) ? 1 : (dx == 0 ? 0 : 2);
-#pragma unroll
-      for (int co = 0; co < 3; ++co) {
-        const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
-        const float* wb = w + ((kyb * 3 + kxb) * 3 + co) * CIN;
-        if constexpr (PK) {
-          f32x2 s2 = {acc[pa][co], acc[pb][co]};
-#pragma unroll
-          for (int ci = 0; ci < CIN; ++ci) {
-            const f32x2 xx = {x[ci], x[ci]};
-            const f32x2 ww = {wa[ci], wb[ci]};
-            s2 = __builtin_elementwise_fma(xx, ww, s2);
-          }
-          acc[pa][co] = s2.x;
-          acc[pb][co] = s2.y;
-        } else {
-          float sa = acc[pa][co], sb = acc[pb][co];
-#pragma unroll
-          for (int ci = 0; ci < CIN; ++ci) {
-            sa = fmaf(x[ci], wa[ci], sa);
-            sb = fmaf(x[ci], wb[ci], sb);
-          }
-          acc[pa][co] = sa;
-          acc[pb][co] = sb;
+        for (int ci = 0; ci < CIN; ++ci) {
+          const f32x2 xx = {x[ci], x[ci]};
+          const f32x2 ww = {wa[ci], wb[ci]};
+          s2 = __builtin_elementwise_fma(xx, ww, s2);
         }
-      }
-    }
-    if (np & 1) {
-      const int pa = ph[np - 1];
-      const int kya = (pa >> 1) ? 1 : (dy == 0 ? 0 : 2), kxa = (pa & 1) ? 1 : (dx == 0 ? 0 : 2);
+        acc[PA][co] = s2.x;
+        acc[PB][co] = s2.y;
+      } else {
+        float sa = acc[PA][co], sb = acc[PB][co];
 #pragma unroll
-      for (int co = 0; co < 3; ++co) {
-        const float* wa = w + ((kya * 3 + kxa) * 3 + co) * CIN;
-#pragma unroll
-        for (int ci = 0; ci < CIN; ++ci) acc[pa][co] = fmaf(x[ci], wa[ci], acc[pa][co]);
+        for (int ci = 0; ci < CIN; ++ci) {
+          sa = fmaf(x[ci], wa[ci], sa);
+          sb = fmaf(x[ci], wb[ci], sb);
+        }
+        acc[PA][co] = sa;
+        acc[PB][co] = sb;
       }
     }
   }
 }
 
-template <int CIN, int PS, int LC>
-__device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, float (&acc)[4][3]) {
-  rgb_out_fma_g<CIN>(
+template <int CIN, bool PK, int OFF, class Ld, class W>
+__device__ __forceinline__ void offset(Ld& ld, W w, f32x4 (&acc)[4]) {
+  float x[CIN];
+#pragma unroll
+  for (int c4 = 0; c4 < CIN / 4; ++c4) {
+    const f32x4 v = ld(-(OFF >> 1), -(OFF & 1), c4);
+    x[4 * c4] = v.x;
+    x[4 * c4 + 1] = v.y;
+    x[4 * c4 + 2] = v.z;
+    x[4 * c4 + 3] = v.w;
+  }
+  // phases paired so one packed fma advances two outputs' chains by one step each — every
+  // output's own fma order is unchanged
+  if constexpr (nphase(OFF) >= 2) chains<CIN, PK, OFF, phase(OFF, 0), phase(OFF, 1)>(x, w, acc);
+  if constexpr (nphase(OFF) == 4) chains<CIN, PK, OFF, phase(OFF, 2), phase(OFF, 3)>(x, w, acc);
+  if constexpr (nphase(OFF) == 1) chains<CIN, PK, OFF, 0, -1>(x, w, acc);
+}
+}  // namespace rgbout
+
+template <int CIN, bool PK = true, bool WG = true, class Ld>
+__device__ __forceinline__ void rgb_out_fma_g(Ld ld, const float* __restrict__ wg, f32x4 (&acc)[4]) {
+  const rgbout::wptr<WG> w = (rgbout::wptr<WG>)wg;
+  rgbout::offset<CIN, PK, 0>(ld, w, acc);
+  rgbout::offset<CIN, PK, 1>(ld, w, acc);
+  rgbout::offset<CIN, PK, 2>(ld, w, acc);
+  rgbout::offset<CIN, PK, 3>(ld, w, acc);
+}
+
+template <int CIN, int PS, int LC, bool WG = true>
+__device__ __forceinline__ void rgb_out_fma(const float* self, const float* __restrict__ w, f32x4 (&acc)[4]) {
+  rgb_out_fma_g<CIN, true, WG>(
       [&](int dy, int dx, int c4) { return *reinterpret_cast<const f32x4*>(self + (dy * LC + dx) * PS + 4 * c4); }, w,
       acc);
 }
 
 // + bias, * std + mean, clip -> LDS output tile row-major [.][OW] f32 at output pixel
 // (2r + py, 2c + px).
-__device__ __forceinline__ void rgb_out_epilogue(const RgbOutArgs& a, const float (&acc)[4][3], float* lout,
+__device__ __forceinline__ void rgb_out_epilogue(const RgbOutArgs& a, const f32x4 (&acc)[4], float* lout,
                                                  int OW, int r, int c) {
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph) {
@@ -227,7 +247,7 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_kernel(const RgbOutArgs a)
   __syncthreads();
 
   const int r = tid / TW, c = tid % TW;
-  float acc[4][3] = {};
+  f32x4 acc[4] = {};  // [phase][co], lane 3 unused
   rgb_out_fma<CIN, PS, LC>(&lds[((r + 1) * LC + (c + 1)) * PS], a.wraw, acc);
   __syncthreads();  // input tile no longer needed: reuse LDS for the output tile
   rgb_out_epilogue(a, acc, lds, 2 * TW * 3, r, c);
@@ -294,8 +314,8 @@ __global__ void __launch_bounds__(256) convT_rgb_valu_persist_kernel(const RgbOu
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) issue(t + gridDim.x);
 
-    float acc[4][3] = {};
-    rgb_out_fma<CIN, PS, LC>(&lin[((r + 1) * LC + (c + 1)) * PS], wsh, acc);
+    f32x4 acc[4] = {};  // [phase][co], lane 3 unused
+    rgb_out_fma<CIN, PS, LC, false>(&lin[((r + 1) * LC + (c + 1)) * PS], wsh, acc);
     rgb_out_epilogue(a, acc, lout, OW, r, c);
     __syncthreads();
 

@@ -143,34 +143,34 @@ static void dec10_t(const Dec10Args& a, int n, hipStream_t s, int v) {
 template <int C1, int C0>
 static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
   const dim3 grid((a.W + 15) / 16, (a.H + 3) / 4, n);
-  switch (variant >> 2) {
-    case 0: dec10_t<C1, C0, 4, false>(a, n, s, variant); break;
-    case 1: dec10_t<C1, C0, 8, false>(a, n, s, variant); break;
-    case 2: dec10_t<C1, C0, 4, true>(a, n, s, variant); break;
-    case 3: dec10_t<C1, C0, 8, true>(a, n, s, variant); break;
-    // timing probes of variant 8 (TIC_DEC10_VARIANT only; results invalid): without decode_1's
-    // MFMAs / decode_0 / the input loads / decode_1's weight loads (dec10.h PROBE)
-    case 4:
-      switch (variant) {
-        case 16: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1, 4, true>), grid, dim3(256), 0, s, a); break;
-        case 17: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2, 4, true>), grid, dim3(256), 0, s, a); break;
-        case 18: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 4, 4, true>), grid, dim3(256), 0, s, a); break;
-        case 19: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 8, 4, true>), grid, dim3(256), 0, s, a); break;
-        default: return false;
-      }
-      break;
+  if (variant < 16) {
+    switch (variant >> 2) {
+      case 0: dec10_t<C1, C0, 4, false>(a, n, s, variant); break;
+      case 1: dec10_t<C1, C0, 8, false>(a, n, s, variant); break;
+      case 2: dec10_t<C1, C0, 4, true>(a, n, s, variant); break;
+      default: dec10_t<C1, C0, 8, true>(a, n, s, variant); break;
+    }
+    return true;
+  }
+  // timing probes of variant 8 (TIC_DEC10_VARIANT only; results invalid): without decode_1's
+  // MFMAs / decode_0 / the input loads / decode_1's weight loads (dec10.h PROBE)
+  switch (variant) {
+    case 100: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 1, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 101: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 102: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 4, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 103: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 8, 4, true>), grid, dim3(256), 0, s, a); break;
     default: return false;
   }
   return true;
 }
 
-// variant bits: 0 decode_0 by packed / plain fmas; 1 decode_1 weight prefetch 2 / 5
-// steps ahead; 2 tiles of 4 / 8 decode_1 input rows; 3 the padded / compact LDS form — all
-// bit-identical
+// variants 0-15, bits: 0 decode_0 by packed / plain fmas; 1 decode_1 weight prefetch 2 / 5
+// steps ahead; 2 tiles of 4 / 8 decode_1 input rows; 3 the padded / compact LDS form.  All
+// bit-identical.
 int dec10_variants() { return 16; }
 
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {
-  if (variant < 0 || variant >= 20) return false;
+  if (variant < 0 || (variant >= dec10_variants() && (variant < 100 || variant > 103))) return false;
   if (c1 == 32 && c0 == 32) return dec10_c<32, 32>(a, n, s, variant);
   if (c1 == 32 && c0 == 16) return dec10_c<32, 16>(a, n, s, variant);
   if (c1 == 64 && c0 == 32) return dec10_c<64, 32>(a, n, s, variant);

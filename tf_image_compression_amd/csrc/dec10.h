@@ -58,19 +58,19 @@ struct Dec10 {
   static_assert(OT <= YT && C1 % 16 == 0 && C0 % 16 == 0 && NCH <= 16, "tile");
 
   // float offset of channel chunk c4 of decode_0 input position pos in yt
-  __device__ static int ychunk(int pos, int c4) {
+  __device__ __forceinline__ static int ychunk(int pos, int c4) {
     if constexpr (CMP) return pos * PSY + 4 * (c4 ^ ((pos / GRP) % NCH));
     else return pos * PSY + 4 * c4;
   }
 
-  __device__ static f32x4 wglob(const Dec10Args& a, int s, int nb, int li, int lg) {
+  __device__ __forceinline__ static f32x4 wglob(const Dec10Args& a, int s, int nb, int li, int lg) {
     const int tap = s / KC, kc = s % KC;
     return *reinterpret_cast<const f32x4*>(a.wp1 + (size_t)(lg * C0 + li) * 4 + (size_t)(tap * KC + kc) * 4 * C0 * 4 +
                                            nb * 64);
   }
 
   // decode_1's input rows m0-1 .. m0+3, columns q0-1 .. q0+15 (zero outside) into registers
-  __device__ static void issue(const Dec10Args& a, f32x4 (&pre)[NIT], int q0, int m0, int nimg, int tid) {
+  __device__ __forceinline__ static void issue(const Dec10Args& a, f32x4 (&pre)[NIT], int q0, int m0, int nimg, int tid) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int e = i * NT + tid;
@@ -83,7 +83,7 @@ struct Dec10 {
       }
     }
   }
-  __device__ static void land(float* xt, const f32x4 (&pre)[NIT], int tid) {
+  __device__ __forceinline__ static void land(float* xt, const f32x4 (&pre)[NIT], int tid) {
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int e = i * NT + tid;
@@ -91,17 +91,11 @@ struct Dec10 {
     }
   }
 
-  // One tile, its input already in xt (and a barrier behind it): decode_1 by MFMA into yt,
-  // the halo, decode_0 on the VALU, the output.  av holds the first PF weight steps on
-  // entry; with `again`, they are reloaded for the next tile right after the K loop.
-  __device__ static void tile(const Dec10Args& a, float* xt, float* yt, const float* wsh, f32x4 (&av)[PF + 1][NB],
-                              int q0, int m0, int nimg, bool again) {
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // decode_1 input row of this wave
-    const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
-
-    // ---- 2. interior: conv3x3_kernel<MODE_T2>'s step order, one input row per wave ----
-    f32x4 acc[4][NB];
+  // ---- 2. decode_1's interior by MFMA: conv3x3_kernel<MODE_T2>'s step order, one input row
+  //         per wave (wave < TA); av holds the first PF weight steps on entry and, with
+  //         `again`, again on exit (the next tile uses the same weights) ----
+  __device__ __forceinline__ static void interior(const Dec10Args& a, const float* xt, f32x4 (&av)[PF + 1][NB], f32x4 (&acc)[4][NB],
+                                  int wave, int li, int lg, bool again) {
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -134,108 +128,133 @@ struct Dec10 {
         }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (again) {  // the next tile's first weight steps (the same weights) fly from here
+    if (again) {
 #pragma unroll
       for (int p = 0; p < PF; ++p)
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) av[p][nb] = wglob(a, p, nb, li, lg);
     }
-    auto put_interior = [&]() {
+  }
+  // + bias, ReLU -> yt
+  __device__ __forceinline__ static void put_interior(const Dec10Args& a, float* yt, const f32x4 (&acc)[4][NB], int wave, int li,
+                                      int lg) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int py = p >> 1, px = p & 1;
+    for (int p = 0; p < 4; ++p) {
+      const int py = p >> 1, px = p & 1;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          const int co = nb * 16 + lg * 4;
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
-          f32x4 v = acc[p][nb];
-          v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
-          v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
-          v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
-          v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
-          *reinterpret_cast<f32x4*>(&yt[ychunk((1 + 2 * wave + py) * LCY + 1 + 2 * li + px, co / 4)]) = v;
-        }
-      }
-    };
-    if constexpr (!CMP) put_interior();
-
-    // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
-    //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
-    //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
-    //         q0-1, rows m0-1 .. m0+TA-1: taps 1, 4, 7; lane j = input row m0-1+j, j <= TA) ----
-    const bool row = wave == 0;
-    f32x4 hacc[2][NB];  // [0]: phase 2 (row) / phase 1 (column); [1]: phase 3
-    if (wave < 2) {
-      f32x4 ha[3 * KC][NB];
-#pragma unroll
-      for (int ti = 0; ti < 3; ++ti)
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
-            ha[ti * KC + kc][nb] = wglob(a, ((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb, li, lg);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ti = 0; ti < 3; ++ti) {
-        const int tap = (row ? 3 : 1) + ti * (row ? 1 : 3);
-        const int q = tap == 4 ? 1 : 0;
-        int lp;
-        if (row) lp = li + 1 - (tap == 5);  // input row m0-1 (LDS row 0), column q0+li (-1 for tap 5)
-        else lp = min(max(li - (tap == 7), 0), LRX - 1) * LCX;  // input column q0-1 (LDS column 0)
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(&xt[lp * PSX + kc * 16 + lg * 4]);
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
-        }
+      for (int nb = 0; nb < NB; ++nb) {
+        const int co = nb * 16 + lg * 4;
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
+        f32x4 v = acc[p][nb];
+        v.x = fmaxf(__fadd_rn(v.x, bb.x), 0.f);
+        v.y = fmaxf(__fadd_rn(v.y, bb.y), 0.f);
+        v.z = fmaxf(__fadd_rn(v.z, bb.z), 0.f);
+        v.w = fmaxf(__fadd_rn(v.w, bb.w), 0.f);
+        *reinterpret_cast<f32x4*>(&yt[ychunk((1 + 2 * wave + py) * LCY + 1 + 2 * li + px, co / 4)]) = v;
       }
     }
-    if constexpr (CMP) {  // xt lives inside yt: every read of it precedes the first write
-      __syncthreads();
-      put_interior();
-    }
-    if (wave < 2) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          const int co = nb * 16 + lg * 4;
-          int ry, cy;
-          bool use;
-          if (row) {
-            ry = 0, cy = 1 + 2 * li + q, use = true;
-          } else {
-            ry = q ? 2 * li : 2 * li - 1, cy = 0, use = q ? li <= TA : (li >= 1 && li <= TA);
-          }
-          if (!use) continue;
-          const bool inside = 2 * m0 - 1 + ry >= 0 && 2 * q0 - 1 + cy >= 0;
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
-          f32x4 v = hacc[q][nb];
-          v.x = inside ? fmaxf(__fadd_rn(v.x, bb.x), 0.f) : 0.f;
-          v.y = inside ? fmaxf(__fadd_rn(v.y, bb.y), 0.f) : 0.f;
-          v.z = inside ? fmaxf(__fadd_rn(v.z, bb.z), 0.f) : 0.f;
-          v.w = inside ? fmaxf(__fadd_rn(v.w, bb.w), 0.f) : 0.f;
-          *reinterpret_cast<f32x4*>(&yt[ychunk(ry * LCY + cy, co / 4)]) = v;
-        }
-    }
-    __syncthreads();
+  }
 
-    // ---- 4. decode_0 on the VALU; output tile staged in the dead decode_1 input tile (or,
-    //         when it is too small, in yt once every thread has read its inputs) ----
-    const int r = tid / TW, c = tid % TW;
-    float acc3[4][3] = {};
+  // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
+  //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
+  //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
+  //         q0-1, rows m0-1 .. m0+TA-1: taps 1, 4, 7; lane j = input row m0-1+j, j <= TA);
+  //         hacc[0]: phase 2 (row) / phase 1 (column), hacc[1]: phase 3 ----
+  __device__ __forceinline__ static void halo(const Dec10Args& a, const float* xt, f32x4 (&hacc)[2][NB], bool row, int li, int lg) {
+    f32x4 ha[3 * KC][NB];
+#pragma unroll
+    for (int ti = 0; ti < 3; ++ti)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          ha[ti * KC + kc][nb] = wglob(a, ((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb, li, lg);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ti = 0; ti < 3; ++ti) {
+      const int tap = (row ? 3 : 1) + ti * (row ? 1 : 3);
+      const int q = tap == 4 ? 1 : 0;
+      int lp;
+      if (row) lp = li + 1 - (tap == 5);  // input row m0-1 (LDS row 0), column q0+li (-1 for tap 5)
+      else lp = min(max(li - (tap == 7), 0), LRX - 1) * LCX;  // input column q0-1 (LDS column 0)
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(&xt[lp * PSX + kc * 16 + lg * 4]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
+      }
+    }
+  }
+  // + bias, ReLU (zero where the position lies above / left of the image: decode_0's zero
+  // padding) -> yt
+  __device__ __forceinline__ static void put_halo(const Dec10Args& a, float* yt, const f32x4 (&hacc)[2][NB], bool row, int li, int lg,
+                                  int q0, int m0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int co = nb * 16 + lg * 4;
+        int ry, cy;
+        bool use;
+        if (row) {
+          ry = 0, cy = 1 + 2 * li + q, use = true;
+        } else {
+          ry = q ? 2 * li : 2 * li - 1, cy = 0, use = q ? li <= TA : (li >= 1 && li <= TA);
+        }
+        if (!use) continue;
+        const bool inside = 2 * m0 - 1 + ry >= 0 && 2 * q0 - 1 + cy >= 0;
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(a.b1 + co);
+        f32x4 v = hacc[q][nb];
+        v.x = inside ? fmaxf(__fadd_rn(v.x, bb.x), 0.f) : 0.f;
+        v.y = inside ? fmaxf(__fadd_rn(v.y, bb.y), 0.f) : 0.f;
+        v.z = inside ? fmaxf(__fadd_rn(v.z, bb.z), 0.f) : 0.f;
+        v.w = inside ? fmaxf(__fadd_rn(v.w, bb.w), 0.f) : 0.f;
+        *reinterpret_cast<f32x4*>(&yt[ychunk(ry * LCY + cy, co / 4)]) = v;
+      }
+  }
+
+  // ---- 4. decode_0 of input position (r, c) of the tile on the VALU (acc3 zeroed) ----
+  __device__ __forceinline__ static void decode0(const Dec10Args& a, const float* yt, const float* wsh, f32x4 (&acc3)[4], int r,
+                                 int c) {
     if constexpr ((PROBE & 2) != 0) acc3[0][0] = yt[((r + 1) * LCY + (c + 1)) * PSY];
     else
-      rgb_out_fma_g<C0, PK>(
+      rgb_out_fma_g<C0, PK, !WSH>(
           [&](int dy, int dx, int c4) {
             return *reinterpret_cast<const f32x4*>(&yt[ychunk((r + 1 + dy) * LCY + c + 1 + dx, c4)]);
           },
           WSH ? wsh : a.rgb.wraw, acc3);
+  }
+
+  // One tile, its input already in xt (and a barrier behind it): decode_1 by MFMA into yt,
+  // the halo, decode_0 on the VALU, the output.
+  __device__ __forceinline__ static void tile(const Dec10Args& a, float* xt, float* yt, const float* wsh, f32x4 (&av)[PF + 1][NB],
+                              int q0, int m0, int nimg) {
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // decode_1 input row of this wave
+    const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
+    f32x4 acc[4][NB];
+    interior(a, xt, av, acc, wave, li, lg, false);
+    if constexpr (!CMP) put_interior(a, yt, acc, wave, li, lg);
+    const bool row = wave == 0;
+    f32x4 hacc[2][NB];
+    if (wave < 2) halo(a, xt, hacc, row, li, lg);
+    if constexpr (CMP) {  // xt lives inside yt: every read of it precedes the first write
+      __syncthreads();
+      put_interior(a, yt, acc, wave, li, lg);
+    }
+    if (wave < 2) put_halo(a, yt, hacc, row, li, lg, q0, m0);
+    __syncthreads();
+
+    // decode_0; output tile staged in the dead decode_1 input tile (or, when it is too small,
+    // in yt once every thread has read its inputs)
+    const int r = tid / TW, c = tid % TW;
+    f32x4 acc3[4] = {};
+    decode0(a, yt, wsh, acc3, r, c);
     float* const ot = OUT_IN_XT ? xt : yt;
     if constexpr (!OUT_IN_XT) __syncthreads();
     rgb_out_epilogue(a.rgb, acc3, ot, 2 * TW * 3, r, c);
@@ -270,7 +289,7 @@ __global__ void __launch_bounds__(64 * TA, CMP ? (TA == 4 ? (WSH ? 3 : 4) : 2) :
     D::land(xt, pre, tid);
   }
   __syncthreads();
-  D::tile(a, xt, yt, wsh, av, q0, m0, nimg, false);
+  D::tile(a, xt, yt, wsh, av, q0, m0, nimg);
 }
 
 }  // namespace tic

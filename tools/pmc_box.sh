@@ -8,7 +8,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1
-TUNE=$2
+TUNE=$(realpath $2)
 shift 2
 O=$R/gpurun_out/pmc_$TAG
 mkdir -p $O
