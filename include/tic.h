@@ -35,6 +35,7 @@ extern "C" {
 #define TIC_EIO (-8)        /* file I/O (reference: IOError / RuntimeError) */
 
 #define TIC_MODEL_RMBE 100  /* submit/2/rmbe/model.py:113 (block-effect post-filter) */
+#define TIC_MODEL_CH128 128 /* base_model/ch_128/model.py:34-215 (128-channel trunk, P/4 code) */
 
 typedef struct tic_handle tic_handle;
 
@@ -46,7 +47,7 @@ const char* tic_last_error(void);
  * Replaces: `from model_N import model` (encode.py:225-232, decode.py:280-287,
  *   submit/encoder.py:220-223) + model_N/config.json's patch_size/quan_scale
  *   (encode.py:129-145) + os.environ['CUDA_VISIBLE_DEVICES']=gpu (encode.py:218).
- * model_id: 0..3 or TIC_MODEL_RMBE.  patch_size: even, >= 16 (for rmbe: 128).
+ * model_id: 0..3, TIC_MODEL_CH128 or TIC_MODEL_RMBE.  patch_size: even, >= 16 (for rmbe: 128).
  * quan_scale: Q in [2, 256] (model_0/config.json:6). */
 int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_handle** out);
 void tic_destroy(tic_handle* h);

@@ -125,6 +125,21 @@ _M3_DEC = [
     ("decode_2", "convT", 64, 32, "relu"),
     ("decode_1", "convT", 32, 3, "identity"),
 ]
+# base_model/ch_128/model.py:50-110 (encoder), :135-200 (decoder): the 128-channel trunk
+_CH128_ENC = [
+    ("encode_1", "conv_s2", 3, 64, "relu"),
+    ("encode_2", "conv_s2", 64, 128, "relu"),
+    ("encode_res_1", "res", 128, 128, "relu"),
+    ("encode_res_2", "res", 128, 128, "relu"),
+    ("encode_3", "conv_s1", 128, 64, "identity"),
+]
+_CH128_DEC = [
+    ("decode_3", "conv_s1", 64, 128, "identity"),
+    ("decode_res_1", "res", 128, 128, "relu"),
+    ("decode_res_2", "res", 128, 128, "relu"),
+    ("decode_2", "convT", 128, 64, "relu"),
+    ("decode_1", "convT", 64, 3, "identity"),
+]
 # submit/2/rmbe/model.py:118-189 (block-effect post-filter)
 RMBE = [
     ("conv_1", "conv_s2", 3, 32, "relu"),
@@ -140,6 +155,7 @@ MODELS = {
     1: (_M1_ENC, _M1_DEC),
     2: (_M2_ENC, _M2_DEC),
     3: (_M3_ENC, _M3_DEC),
+    128: (_CH128_ENC, _CH128_DEC),  # base_model/ch_128
 }
 
 # model_N/config.json (patch_size, quan_scale); model_2/3 use 128 (model_3/config.json:5)

@@ -58,7 +58,7 @@ def _native_table(L, model_id):
     return out
 
 
-@pytest.mark.parametrize("model_id", [0, 1, 2, 3, 100])
+@pytest.mark.parametrize("model_id", [0, 1, 2, 3, 128, 100])
 def test_native_table_matches_host_and_oracle(L, model_id):
     from tf_image_compression_amd.topology import layer_table
     kinds = {"conv_s1": 0, "conv_s2": 1, "convT": 2}

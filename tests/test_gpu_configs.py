@@ -270,3 +270,43 @@ def test_lane_decoupling_orders_stream_work(decouple):
             assert np.array_equal(got1.astype(np.int64), np.histogram(ref1, [0, 1, 2])[0])
             assert np.array_equal(d_idx.download(ref2.shape, np.uint8), ref2)
         c.set_option("streams", 2)
+
+
+@pytest.mark.parametrize("P", [64, 128])
+def test_codec_ch128(P):
+    """base_model/ch_128 (channel width 128): the 64 -> 128 stride-2
+    layer, the 128-wide residual stages (direct and Winograd forms), the 128 -> 64
+    quantiser layer, the 64 -> 128 dequantiser layer and the 128 -> 64 / 64 -> 3 transposed
+    convs, against the oracle; code P/4 x P/4 x 64 (base_model/ch_128/model.py:34-215)."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.topology import CH128_ID
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    params = synthetic_params(CH128_ID, seed=0)
+    with Codec(CH128_ID, params, SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
+        assert c.code_shape == (P // 4, P // 4, 64)
+        x = structured_patches(2, P, seed=900 + P)
+        idx, rgb = check_codec(c, params, CH128_ID, P, x)
+        c.set_option("s1_form", 0)  # the direct form of the 128-wide stride-1 layers
+        check_codec(c, params, CH128_ID, P, x)
+
+
+def test_ch128_model_module():
+    """The drop-in module path of base_model/ch_128: encoder / decoder as the reference's
+    (base_model/ch_128/model.py:34,123), patch size recovered from the code shape."""
+    from tf_image_compression_amd.base_model.ch_128 import model
+    from tf_image_compression_amd.topology import CH128_ID
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    params = synthetic_params(CH128_ID, seed=0)
+    model.restore(params, SYNTH_MEAN, SYNTH_STD)
+    try:
+        x = structured_patches(2, 128, seed=910)
+        sym = model.encoder(x, 128, 2)
+        assert sym.shape == (2, 32, 32, 64)
+        ref_pre, ref_idx = o.encoder(params, SYNTH_MEAN, SYNTH_STD, x, 128, 2, CH128_ID)
+        safe = o.decision_margin(ref_pre, 2) > 1e-5 * max(1.0, float(np.max(np.abs(ref_pre))))
+        assert int(np.count_nonzero((sym != ref_idx) & safe)) == 0
+        f = model.decoder(sym, 2)
+        ref_f, _ = o.decoder(params, SYNTH_MEAN, SYNTH_STD, sym, 2, CH128_ID)
+        assert f.shape == (2, 128, 128, 3) and float(np.max(np.abs(f - ref_f))) <= 1e-2
+    finally:
+        model._module.close()

@@ -13,7 +13,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check, ptr, lib
-from .topology import RMBE_ID, param_shapes
+from .topology import CH128_ID, RMBE_ID, param_shapes
 
 F32 = np.float32
 
@@ -54,7 +54,7 @@ class Codec:
                  quan_scale: int = 2, device: int = 0):
         self.model_id = int(model_id)
         if patch_size is None:
-            patch_size = 128 if model_id in (2, 3, RMBE_ID) else 256
+            patch_size = 128 if model_id in (2, 3, CH128_ID, RMBE_ID) else 256
         self.patch_size = int(patch_size)
         self.quan_scale = int(quan_scale)
         self.device = int(device)

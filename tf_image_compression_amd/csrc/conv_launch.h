@@ -42,6 +42,11 @@ static void launch_conv_persist(const ConvArgs& a, int n, hipStream_t s) {
 #define TIC_CONV(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT)            \
   TIC_CONVW(MODE, CIN, COUT, TH, WR, NSPLIT, 0, ACT, RES, IN, OUT),              \
       TIC_CONVW(MODE, CIN, COUT, TH, WR, NSPLIT, 1, ACT, RES, IN, OUT)
+// the two L2 weight sources (PF 2 / deep prefetch) — 128-wide layers, whose per-tap slab
+// (64 KB at 128 x 128) does not fit a 2-slot LDS ring beside the input tile
+#define TIC_CONVL2(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT)          \
+  TIC_CONVW(MODE, CIN, COUT, TH, WR, NSPLIT, 0, ACT, RES, IN, OUT),              \
+      TIC_CONVW(MODE, CIN, COUT, TH, WR, NSPLIT, 2, ACT, RES, IN, OUT)
 // all three weight sources (small grids: + L2 with deep prefetch)
 #define TIC_CONV3(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT)           \
   TIC_CONV(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT),                  \

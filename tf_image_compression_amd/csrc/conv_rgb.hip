@@ -32,6 +32,7 @@ static bool rgb_in_c(bool u8_input, const RgbInArgs& a, int n, hipStream_t s, in
 }
 
 bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant) {
+  if (cout == 64) return rgb_in_c<64>(u8_input, a, n, s, variant);  // base_model/ch_128 encode_1
   if (cout == 32) return rgb_in_c<32>(u8_input, a, n, s, variant);
   if (cout == 16) return rgb_in_c<16>(u8_input, a, n, s, variant);
   return false;
@@ -122,6 +123,7 @@ static bool rgb_out_c(const RgbOutArgs& a, int n, hipStream_t s, int variant) {
 }
 
 bool launch_rgb_out(int cin, const RgbOutArgs& a, int n, hipStream_t s, int variant) {
+  if (cin == 64) return rgb_out_c<64>(a, n, s, variant);  // base_model/ch_128 decode_1
   if (cin == 32) return rgb_out_c<32>(a, n, s, variant);
   if (cin == 16) return rgb_out_c<16>(a, n, s, variant);
   return false;

@@ -26,6 +26,16 @@
       TIC_WINO(64, 64, 2, 2, 1, ACT, RES, IN, OUT),         \
       TIC_WINO(64, 64, 4, 2, 1, ACT, RES, IN, OUT)
 
+// base_model/ch_128: the 128-wide res-block convs, encode_3 (128 -> 64, quantiser) and
+// decode_3 (64 -> 128, dequantiser), direct and Winograd
+#define S1_128(CIN, COUT, ACT, RES, IN, OUT)                           \
+  TIC_CONVL2(MODE_S1, CIN, COUT, 4, 4, 2, ACT, RES, IN, OUT),          \
+      TIC_CONVL2(MODE_S1, CIN, COUT, 2, 2, 2, ACT, RES, IN, OUT),      \
+      TIC_CONVL2(MODE_S1, CIN, COUT, 4, 4, 4, ACT, RES, IN, OUT),      \
+      TIC_WINO(CIN, COUT, 2, 1, 2, ACT, RES, IN, OUT),                 \
+      TIC_WINO(CIN, COUT, 2, 1, 4, ACT, RES, IN, OUT),                 \
+      TIC_WINO(CIN, COUT, 1, 1, 4, ACT, RES, IN, OUT)
+
 namespace tic {
 static const ConvEntry kS1[] = {
     S1_VARIANTS(ACT_RELU, false, IN_F32, OUT_F32),
@@ -38,6 +48,10 @@ static const ConvEntry kS1[] = {
     S1_WINO(ACT_ID, false, IN_F32, OUT_QUANT),
     S1_WINO(ACT_ID, false, IN_IDX, OUT_F32),
     S1_WINO(ACT_ID, false, IN_F32, OUT_F32),
+    S1_128(128, 128, ACT_RELU, false, IN_F32, OUT_F32),
+    S1_128(128, 128, ACT_RELU, true, IN_F32, OUT_F32),
+    S1_128(128, 64, ACT_ID, false, IN_F32, OUT_QUANT),
+    S1_128(64, 128, ACT_ID, false, IN_IDX, OUT_F32),
 };
 const ConvEntry* conv_registry_s1(int* count) {
   *count = sizeof(kS1) / sizeof(kS1[0]);

@@ -22,6 +22,10 @@ static const ConvEntry kT2[] = {
     TIC_CONV(MODE_T2, 80, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 80, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONV(MODE_T2, 64, 64, 4, 4, 1, ACT_ID, false, IN_F32, OUT_F32),
+    // base_model/ch_128 decode_2 (128 -> 64)
+    TIC_CONVL2(MODE_T2, 128, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONVL2(MODE_T2, 128, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
+    TIC_CONVL2(MODE_T2, 128, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_PERSIST(MODE_T2, 32, 32, 4, 4, ACT_RELU),
     TIC_PERSIST(MODE_T2, 32, 32, 8, 4, ACT_RELU),
     TIC_PERSIST(MODE_T2, 32, 16, 4, 4, ACT_RELU),

@@ -136,6 +136,15 @@ bool model_table(int model_id, std::vector<LayerDef>* out) {
                    {"decode_2", K_T2, 64, 32, R}, {"decode_1", K_T2, 32, 3, I}});
     return true;
   }
+  if (model_id == TIC_MODEL_CH128) {  // base_model/ch_128/model.py:50-110 (encoder), :135-200 (decoder)
+    *out = expand({{"encode_1", K_S2, 3, 64, R}, {"encode_2", K_S2, 64, 128, R},
+                   {"encode_res_1", RES, 128, 128, R}, {"encode_res_2", RES, 128, 128, R},
+                   {"encode_3", K_S1, 128, 64, I}},
+                  {{"decode_3", K_S1, 64, 128, I},
+                   {"decode_res_1", RES, 128, 128, R}, {"decode_res_2", RES, 128, 128, R},
+                   {"decode_2", K_T2, 128, 64, R}, {"decode_1", K_T2, 64, 3, I}});
+    return true;
+  }
   if (model_id == TIC_MODEL_RMBE) {  // submit/2/rmbe/model.py:118-189
     *out = expand({{"conv_1", K_S2, 3, 32, R}, {"conv_2", K_S2, 32, 64, R},
                    {"conv_3", K_S1, 64, 64, R}, {"conv_4", K_S1, 64, 64, R}},
@@ -570,8 +579,10 @@ struct Prof {
 
 // encode_0 -> encode_1 through one enc01_kernel launch (opt-in "fuse01")
 static bool fuses01(const tic_handle* h) {
-  return h->fuse01 && h->layers.size() > 2 && h->layers[1].def.kind == K_S2 && h->layers[1].def.act == 1 &&
-         !h->layers[1].def.residual && !(!h->rmbe() && h->n_enc == 2);
+  if (!h->fuse01 || h->layers.size() <= 2) return false;
+  const LayerDef& d = h->layers[1].def;
+  const bool ok = (d.cin == 32 && d.cout == 32) || (d.cin == 16 && d.cout == 32) || (d.cin == 32 && d.cout == 64);
+  return ok && d.kind == K_S2 && d.act == 1 && !d.residual && !(!h->rmbe() && h->n_enc == 2);
 }
 
 // decoder's last two layers through one dec10_kernel launch (option "fuse_tail"; only with
@@ -1031,7 +1042,8 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (!out) return fail(TIC_EINVAL, "null output handle pointer");
   *out = nullptr;
   std::vector<LayerDef> table;
-  if (!model_table(model_id, &table)) return fail(TIC_EINVAL, "unknown model id %d (expected 0..3 or %d)", model_id, TIC_MODEL_RMBE);
+  if (!model_table(model_id, &table)) return fail(TIC_EINVAL, "unknown model id %d (expected 0..3, %d or %d)", model_id,
+                                                TIC_MODEL_CH128, TIC_MODEL_RMBE);
   if (patch_size < 16 || patch_size % 2 != 0 || patch_size > 8192)
     return fail(TIC_EINVAL, "patch_size %d must be even and in [16, 8192]", patch_size);
   if (quan_scale < 2 || quan_scale > 256) return fail(TIC_EINVAL, "quan_scale %d must be in [2, 256]", quan_scale);

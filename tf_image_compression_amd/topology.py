@@ -7,7 +7,8 @@ host-side mirror used for weight names/shapes and roofline accounting, and
 independently written tables).
 
 Sources: model_0/model.py:50-246, model_1/model.py (widths 16 at :52/:226),
-model_2/model.py:50-193, model_3/model.py:50-300, submit/2/rmbe/model.py:118-189.
+model_2/model.py:50-193, model_3/model.py:50-300, base_model/ch_128/model.py:50-200,
+submit/2/rmbe/model.py:118-189.
 ``res_block`` (basic_block/basic_block.py:74-93) expands into ``<scope>/conv_0`` and
 ``<scope>/conv_1`` (both ReLU); the block input is added after conv_1 (no activation).
 """
@@ -16,6 +17,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 RMBE_ID = 100  # pseudo model id for the submit/2 block-effect post-filter
+CH128_ID = 128  # base_model/ch_128: the 128-channel trunk (include/tic.h TIC_MODEL_CH128)
+MODEL_IDS = (0, 1, 2, 3, CH128_ID, RMBE_ID)
 
 
 @dataclass(frozen=True)
@@ -67,6 +70,14 @@ def _blocks(model_id):
                ("decode_3", "convT", 64, 64, r),
                ("decode_res_4", "res", 64, 64, r), ("decode_res_5", "res", 64, 64, r),
                ("decode_2", "convT", 64, 32, r), ("decode_1", "convT", 32, 3, i)]
+        return enc, dec
+    if model_id == CH128_ID:
+        enc = [("encode_1", "conv_s2", 3, 64, r), ("encode_2", "conv_s2", 64, 128, r),
+               ("encode_res_1", "res", 128, 128, r), ("encode_res_2", "res", 128, 128, r),
+               ("encode_3", "conv_s1", 128, 64, i)]
+        dec = [("decode_3", "conv_s1", 64, 128, i),
+               ("decode_res_1", "res", 128, 128, r), ("decode_res_2", "res", 128, 128, r),
+               ("decode_2", "convT", 128, 64, r), ("decode_1", "convT", 64, 3, i)]
         return enc, dec
     if model_id == RMBE_ID:
         enc = [("conv_1", "conv_s2", 3, 32, r), ("conv_2", "conv_s2", 32, 64, r),
