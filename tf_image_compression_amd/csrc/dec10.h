@@ -49,6 +49,9 @@ struct Dec10 {
   static constexpr int YT = LRY * LCY * PSY;        // decode_0 input tile incl. halo (floats)
   static constexpr int OT = 2 * TH * 2 * TW * 3;    // decode_0 output staging (floats)
   static constexpr int NB = C0 / 16;
+  // the halo's MFMA passes: row / column x output-channel halves over 4 waves when there are
+  // two channel blocks (each wave 1/4 of the halo), else row / column on waves 0 / 1
+  static constexpr int HS = (NB % 2 == 0 && TA >= 4) ? 2 : 1, HNB = NB / HS, HW = 2 * HS;
   static constexpr int NSTEP = 9 * KC;
   static constexpr int NSTAGE = LRX * LCX * C4;
   static constexpr int NIT = (NSTAGE + NT - 1) / NT;
@@ -158,21 +161,23 @@ struct Dec10 {
   // ---- 3. the halo by MFMA, in conv3x3_kernel's order for those outputs (taps ascending,
   //         then chunk, then t): wave 0 the row above the tile (phases 2 and 3 of input row
   //         m0-1: taps 3, 4, 5), wave 1 the column left of it (phases 1 and 3 of input column
-  //         q0-1, rows m0-1 .. m0+TA-1: taps 1, 4, 7; lane j = input row m0-1+j, j <= TA);
-  //         hacc[0]: phase 2 (row) / phase 1 (column), hacc[1]: phase 3 ----
-  __device__ __forceinline__ static void halo(const Dec10Args& a, const float* xt, f32x4 (&hacc)[2][NB], bool row, int li, int lg) {
-    f32x4 ha[3 * KC][NB];
+  //         q0-1, rows m0-1 .. m0+TA-1: taps 1, 4, 7; lane j = input row m0-1+j, j <= TA),
+  //         channel blocks nb0 .. nb0+HNB-1; hacc[0]: phase 2 (row) / phase 1 (column),
+  //         hacc[1]: phase 3 ----
+  __device__ __forceinline__ static void halo(const Dec10Args& a, const float* xt, f32x4 (&hacc)[2][HNB], bool row,
+                                              int nb0, int li, int lg) {
+    f32x4 ha[3 * KC][HNB];
 #pragma unroll
     for (int ti = 0; ti < 3; ++ti)
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          ha[ti * KC + kc][nb] = wglob(a, ((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb, li, lg);
+        for (int nb = 0; nb < HNB; ++nb)
+          ha[ti * KC + kc][nb] = wglob(a, ((row ? 3 : 1) + ti * (row ? 1 : 3)) * KC + kc, nb0 + nb, li, lg);
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nb = 0; nb < HNB; ++nb) hacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ti = 0; ti < 3; ++ti) {
       const int tap = (row ? 3 : 1) + ti * (row ? 1 : 3);
@@ -186,19 +191,19 @@ struct Dec10 {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
+          for (int nb = 0; nb < HNB; ++nb) hacc[q][nb] = mfma4(ha[ti * KC + kc][nb][t], b[t], hacc[q][nb]);
       }
     }
   }
   // + bias, ReLU (zero where the position lies above / left of the image: decode_0's zero
   // padding) -> yt
-  __device__ __forceinline__ static void put_halo(const Dec10Args& a, float* yt, const f32x4 (&hacc)[2][NB], bool row, int li, int lg,
-                                  int q0, int m0) {
+  __device__ __forceinline__ static void put_halo(const Dec10Args& a, float* yt, const f32x4 (&hacc)[2][HNB], bool row,
+                                                  int nb0, int li, int lg, int q0, int m0) {
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const int co = nb * 16 + lg * 4;
+      for (int nb = 0; nb < HNB; ++nb) {
+        const int co = (nb0 + nb) * 16 + lg * 4;
         int ry, cy;
         bool use;
         if (row) {
@@ -240,14 +245,15 @@ struct Dec10 {
     f32x4 acc[4][NB];
     interior(a, xt, av, acc, wave, li, lg, false);
     if constexpr (!CMP) put_interior(a, yt, acc, wave, li, lg);
-    const bool row = wave == 0;
-    f32x4 hacc[2][NB];
-    if (wave < 2) halo(a, xt, hacc, row, li, lg);
+    const bool row = (wave & 1) == 0;
+    const int nb0 = (wave >> 1) * HNB;
+    f32x4 hacc[2][HNB];
+    if (wave < HW) halo(a, xt, hacc, row, nb0, li, lg);
     if constexpr (CMP) {  // xt lives inside yt: every read of it precedes the first write
       __syncthreads();
       put_interior(a, yt, acc, wave, li, lg);
     }
-    if (wave < 2) put_halo(a, yt, hacc, row, li, lg, q0, m0);
+    if (wave < HW) put_halo(a, yt, hacc, row, nb0, li, lg, q0, m0);
     __syncthreads();
 
     // decode_0; output tile staged in the dead decode_1 input tile (or, when it is too small,
