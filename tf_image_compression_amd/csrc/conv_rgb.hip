@@ -161,6 +161,10 @@ static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
     case 101: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 2, 4, true>), grid, dim3(256), 0, s, a); break;
     case 102: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 4, 4, true>), grid, dim3(256), 0, s, a); break;
     case 103: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 8, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 104: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 3, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 105: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 3 | 32, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 106: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 3 | 32 | 16, 4, true>), grid, dim3(256), 0, s, a); break;
+    case 107: hipLaunchKernelGGL((dec10_kernel<C1, C0, false, 2, 3 | 32 | 16 | 4, 4, true>), grid, dim3(256), 0, s, a); break;
     default: return false;
   }
   return true;
@@ -172,7 +176,7 @@ static bool dec10_c(const Dec10Args& a, int n, hipStream_t s, int variant) {
 int dec10_variants() { return 16; }
 
 bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int variant) {
-  if (variant < 0 || (variant >= dec10_variants() && (variant < 100 || variant > 103))) return false;
+  if (variant < 0 || (variant >= dec10_variants() && (variant < 100 || variant > 107))) return false;
   if (c1 == 32 && c0 == 32) return dec10_c<32, 32>(a, n, s, variant);
   if (c1 == 32 && c0 == 16) return dec10_c<32, 16>(a, n, s, variant);
   if (c1 == 64 && c0 == 32) return dec10_c<64, 32>(a, n, s, variant);

@@ -28,7 +28,8 @@ namespace tic {
 // addresses from memory (scalar loads), as the two convT_rgb_valu kernels do.  PF: how many
 // K steps ahead decode_1's weights are loaded (one step = 8 MFMAs = 256 cycles).  PROBE:
 // timing experiments only, a mask of work left out (results invalid): 1 decode_1's MFMAs,
-// 2 decode_0, 4 the input tile's loads, 8 decode_1's weight loads.
+// 2 decode_0, 4 the input tile's loads, 8 decode_1's weight loads, 16 the output store,
+// 32 the halo.
 // CMP: the compact LDS form — decode_0's input tile unpadded (C0 floats per position, its
 // 16-byte chunks XOR-swizzled per position so the ds_read_b128 of 16 consecutive positions
 // still hits 16 distinct bank slots) with decode_1's input tile aliased into it (a barrier
@@ -248,12 +249,12 @@ struct Dec10 {
     const bool row = (wave & 1) == 0;
     const int nb0 = (wave >> 1) * HNB;
     f32x4 hacc[2][HNB];
-    if (wave < HW) halo(a, xt, hacc, row, nb0, li, lg);
+    if (!(PROBE & 32) && wave < HW) halo(a, xt, hacc, row, nb0, li, lg);
     if constexpr (CMP) {  // xt lives inside yt: every read of it precedes the first write
       __syncthreads();
       put_interior(a, yt, acc, wave, li, lg);
     }
-    if (wave < HW) put_halo(a, yt, hacc, row, nb0, li, lg, q0, m0);
+    if (!(PROBE & 32) && wave < HW) put_halo(a, yt, hacc, row, nb0, li, lg, q0, m0);
     __syncthreads();
 
     // decode_0; output tile staged in the dead decode_1 input tile (or, when it is too small,
@@ -265,7 +266,7 @@ struct Dec10 {
     if constexpr (!OUT_IN_XT) __syncthreads();
     rgb_out_epilogue(a.rgb, acc3, ot, 2 * TW * 3, r, c);
     __syncthreads();
-    rgb_out_store<TH, TW, NT>(a.rgb, ot, tid, 2 * m0, 2 * q0, nimg);
+    if constexpr (!(PROBE & 16)) rgb_out_store<TH, TW, NT>(a.rgb, ot, tid, 2 * m0, 2 * q0, nimg);
   }
 };
 

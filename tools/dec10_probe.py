@@ -1,7 +1,8 @@
 """Where does dec10_kernel's time go?  HIP-event timing of the fused decoder tail of
 model_0 (256x256, 32 patches per launch) per variant, including two timing probes whose
 results are invalid (variant 8 without: 100 decode_1's MFMAs, 101 decode_0, 102 the input
-tile loads, 103 decode_1's weight loads)."""
+tile loads, 103 decode_1's weight loads; 104 neither MFMAs nor decode_0, 105 nor the halo,
+106 nor the output store, 107 nor the input loads — an empty tile walk)."""
 import json
 import os
 import subprocess
@@ -32,6 +33,6 @@ if __name__ == "__main__":
         child(int(sys.argv[1]), int(sys.argv[2]))
     else:
         for n in (32, 64):
-            for v in (0, 8, 9, 12, 100, 101, 102, 103):
+            for v in (0, 8, 9, 12, 100, 101, 102, 103, 104, 105, 106, 107):
                 env = dict(os.environ, TIC_DEC10_VARIANT=str(v))
                 subprocess.run([sys.executable, __file__, str(v), str(n)], env=env, check=True, timeout=120)
