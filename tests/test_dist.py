@@ -79,3 +79,31 @@ def test_unique_id_bytes_keep_zeros():
     assert dist.uid_to_bytes(uid) == raw
     with pytest.raises(ValueError):
         dist.uid_from_bytes(raw[:-1])
+
+
+def _uid_peer(rank, world, port, q):
+    from tf_image_compression_amd.dist import exchange_unique_id
+    payload = bytes([0, 7, 0, 0, 255] + list(range(123))) if rank == 0 else None
+    q.put((rank, exchange_unique_id(rank, world, payload, "127.0.0.1", port, timeout=60.0)))
+
+
+def test_unique_id_exchange_world3():
+    """The ncclUniqueId bootstrap of RcclComm (dist.exchange_unique_id): rank 0 serves the
+    128 bytes over TCP and every peer — started before or after the server — receives them
+    intact, zero bytes included (the RCCL path of an N>1 bench run, without a GPU)."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:  # a free port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_uid_peer, args=(r, 3, port, q)) for r in (2, 1, 0)]  # peers first
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=90) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert len(got[0]) == 128 and got[0][:5] == bytes([0, 7, 0, 0, 255])
+    assert got[1] == got[0] and got[2] == got[0]

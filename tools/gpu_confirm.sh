@@ -1,6 +1,8 @@
+# quick bench probes: bash tools/gpu_confirm.sh <tag> [bench args...]
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1
+shift
 cd $R
 mkdir -p gpurun_out
 source tools/gpu_steps.sh
-step confirm_m0 400 python bench.py
-step confirm_m3 400 python bench.py --model 3 --batch 256 --no-cpu-baseline
+step q_$TAG 400 python bench.py --no-cpu-baseline "$@"
