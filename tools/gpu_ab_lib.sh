@@ -1,15 +1,23 @@
-# A/B of two builds of libtic (TIC_LIB) on the default bench and configs[2], alternating.
-set -e
+# A/B of two builds of libtic (TIC_LIB: exp_libs/libtic_base.so vs the tree's) on the default
+# bench and configs[2], alternating on one box, both replaying ONE tuning state (tuned with
+# the tree's build first) so that only the kernels differ:  bash tools/gpu_ab_lib.sh <tag>
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-ab}
 cd $R
 mkdir -p gpurun_out
+source tools/gpu_steps.sh
+O=$R/gpurun_out
+step abt0_$TAG 400 python bench.py --no-cpu-baseline --tune-cache $O/abtune0_$TAG.json --steps 20
+step abt3_$TAG 400 python bench.py --no-cpu-baseline --model 3 --batch 256 --tune-cache $O/abtune3_$TAG.json --steps 5
+for round in 1 2 3; do
+  for v in base new; do
+    if [ $v = new ]; then L=$R/tf_image_compression_amd/libtic.so; else L=$R/exp_libs/libtic_base.so; fi
+    step ab0_${v}_${round}_$TAG 300 env TIC_LIB=$L python bench.py --no-cpu-baseline --tune-cache $O/abtune0_$TAG.json
+  done
+done
 for round in 1 2; do
-for v in base new; do
-  if [ $v = new ]; then L=$R/tf_image_compression_amd/libtic.so; else L=$R/exp_libs/libtic_base.so; fi
-  TIC_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --layers-out gpurun_out/abl_${v}_$round.json > gpurun_out/ab_${v}_$round.json 2> gpurun_out/ab_${v}_$round.err
-done
-done
-for v in base new; do
-  if [ $v = new ]; then L=$R/tf_image_compression_amd/libtic.so; else L=$R/exp_libs/libtic_base.so; fi
-  TIC_LIB=$L timeout -k 10 300 python bench.py --model 3 --batch 256 --no-cpu-baseline --layers-out gpurun_out/abl3_${v}.json > gpurun_out/ab3_${v}.json 2> gpurun_out/ab3_${v}.err
+  for v in base new; do
+    if [ $v = new ]; then L=$R/tf_image_compression_amd/libtic.so; else L=$R/exp_libs/libtic_base.so; fi
+    step ab3_${v}_${round}_$TAG 400 env TIC_LIB=$L python bench.py --no-cpu-baseline --model 3 --batch 256 --tune-cache $O/abtune3_$TAG.json
+  done
 done
