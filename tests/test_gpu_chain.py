@@ -37,14 +37,17 @@ def test_wino_chain_bit_identical(model_id, P, n):
         ref = _run(c, x)
         assert not any("wino_chain" in k for k in c.layer_kernels(n))
         c.set_option("chain", 1)
-        kern = c.layer_kernels(n)
-        assert any(k.startswith("wino_chain_kernel") for k in kern), kern
-        got = _run(c, x)
-        for a, b in zip(ref, got):
-            assert np.array_equal(a, b)
-        # lanes split the batch: chain launches on two streams at once
-        c.set_option("streams", 2)
-        assert all(np.array_equal(a, b) for a, b in zip(ref, _run(c, x)))
+        for wh in (1, 2):  # 256- and 512-thread workgroups
+            c.set_option("chain_wh", wh)
+            c.set_option("streams", 1)
+            kern = c.layer_kernels(n)
+            assert any(k.startswith("wino_chain_kernel") and k.endswith(f",{wh}>") for k in kern), kern
+            got = _run(c, x)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b)
+            # lanes split the batch: chain launches on two streams at once
+            c.set_option("streams", 2)
+            assert all(np.array_equal(a, b) for a, b in zip(ref, _run(c, x)))
         c.set_option("chain", 0)
 
 
@@ -60,11 +63,13 @@ def test_wino_chain_oversubscribed_grid():
         ref_u8 = c.decode(ref_idx)
         c.set_option("chain", 1)
         c.set_option("chunk", 512)
-        for _ in range(3):
-            idx = c.encode(big)
-            assert all(np.array_equal(idx[i * 8:(i + 1) * 8], ref_idx) for i in range(64))
-        u8 = c.decode(idx)
-        assert all(np.array_equal(u8[i * 8:(i + 1) * 8], ref_u8) for i in range(64))
+        for wh in (2, 1):
+            c.set_option("chain_wh", wh)
+            for _ in range(3):
+                idx = c.encode(big)
+                assert all(np.array_equal(idx[i * 8:(i + 1) * 8], ref_idx) for i in range(64))
+            u8 = c.decode(idx)
+            assert all(np.array_equal(u8[i * 8:(i + 1) * 8], ref_u8) for i in range(64))
         c.set_option("chain", 0)
 
 
@@ -98,7 +103,7 @@ def test_wino_chain_device_path_and_tuning_replay():
         assert np.array_equal(d_idx.download(idx.shape, np.uint8), idx)
         assert np.array_equal(d_rgb.download(x.shape, np.uint8), u8)
         text = c.tuning_export()
-        assert "flag chain 1" in text
+        assert "flag chain 1" in text and "flag chain_wh " in text
         with _codec(0, P) as c2:
             c2.tuning_import(text)
             assert c2.tuning_export() == text

@@ -392,6 +392,7 @@ struct tic_handle {
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
+  int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
   // Lane scheduling: lanes join into `stream` after every call, but wait on it (fork) only
   // when something else was enqueued there since their last fork ("decouple"), so lane k's
   // next batch starts as soon as lane k is free instead of after the slowest lane.
@@ -635,6 +636,10 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
   const int L = (int)h->layers.size();
   int cur = -1;       // ws index holding the current activation (-1: external input)
   int block_in = -1;  // ws index of the enclosing res_block's input
+  // timing probe only (results invalid): TIC_PROBE_SKIP = bit mask of plain-conv layers
+  // whose launch is left out, to price a group of layers inside the whole step
+  unsigned long long probe_skip = 0;
+  if (const char* s = getenv("TIC_PROBE_SKIP")) probe_skip = strtoull(s, nullptr, 0);
   for (int li = l0; li < l1; ++li) {
     LayerRT& lay = h->layers[li];
     const LayerDef& d = lay.def;
@@ -760,7 +765,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.ctl = ln.ctl;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
-                                  st))
+                                  st, h->chain_wh))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);
       rc = check_launch();
       if (rc) return rc;
@@ -884,7 +889,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         lay.tuned[tkey(h, lay, n)] = e;
       }
       a.wp = conv_weights(lay, e);
-      e->fn(a, n, st);
+      if (!(li < 64 && (probe_skip >> li & 1))) e->fn(a, n, st);
     }
     int rc = check_launch();
     if (rc) return rc;
@@ -1089,6 +1094,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   else h->fuse_tail = kFuseTailDefault;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
+  if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = atoi(f) == 1 ? 1 : 2;
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) {
@@ -1399,6 +1405,13 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->chain = value != 0;
     return TIC_OK;
   }
+  if (k == "chain_wh") {  // wino_chain_kernel workgroup: 1 = 256 threads, 2 = 512 threads
+    if (value != 1 && value != 2) return fail(TIC_EINVAL, "chain_wh must be 1 or 2");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->chain_wh = value;
+    return TIC_OK;
+  }
   if (k == "s1_form") {  // 0 direct, 1 Winograd, -1 the default (TIC_S1_FORM or built-in)
     if (value < -1 || value > 1) return fail(TIC_EINVAL, "s1_form must be -1, 0 or 1");
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1645,9 +1658,10 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     const char* env;
     const char* name;
   };
-  const Flag flags[3] = {{&h->chain, any_chain, "TIC_CHAIN", "chain"},
-                         {&h->fuse_tail, fuses_tail, "TIC_FUSE_TAIL", "fuse_tail"},
-                         {&h->fuse01, fuses01, "TIC_FUSE01", "fuse01"}};
+  // (the chain last: whether it pays depends on what the fused kernels beside it cost)
+  const Flag flags[3] = {{&h->fuse_tail, fuses_tail, "TIC_FUSE_TAIL", "fuse_tail"},
+                         {&h->fuse01, fuses01, "TIC_FUSE01", "fuse01"},
+                         {&h->chain, any_chain, "TIC_CHAIN", "chain"}};
   for (const Flag& f : flags) {
     if (rc || getenv(f.env)) continue;
     const bool was = *f.v;
@@ -1662,6 +1676,17 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     if (log && !rc) fprintf(stderr, "tune-step %s=%d : %.2f us\n", f.name, (int)*f.v, 1e3f * alt);
     if (!rc && alt < cur) cur = alt;
     else *f.v = was;
+    clear_graphs(h);
+  }
+  if (!rc && h->chain && any_chain(h) && !getenv("TIC_CHAIN_WH")) {  // the chain's workgroup shape
+    const int was = h->chain_wh;
+    h->chain_wh = 3 - was;
+    clear_graphs(h);
+    float alt = 0.f;
+    rc = measure(&alt);
+    if (log && !rc) fprintf(stderr, "tune-step chain_wh=%d : %.2f us\n", h->chain_wh, 1e3f * alt);
+    if (!rc && alt < cur) cur = alt;
+    else h->chain_wh = was;
     clear_graphs(h);
   }
   const int L = (int)h->layers.size();
@@ -1796,7 +1821,7 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     if (cs == i) {
       const int ce = chain_end(h, cs);
       const bool first_dec = !h->rmbe() && cs == h->n_enc, last_enc = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0);
+      snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh);
     }
   } else if (fuses_tail(h) && i >= L - 2) {
     if (i == L - 2) {
@@ -1861,6 +1886,7 @@ int tic_tuning_export(const tic_handle* h, char* buf, int cap) {
   t += "flag fuse_tail " + std::to_string((int)h->fuse_tail) + "\n";
   t += "flag s1_form " + std::to_string(h->s1_form) + "\n";
   t += "flag chain " + std::to_string((int)h->chain) + "\n";
+  t += "flag chain_wh " + std::to_string(h->chain_wh) + "\n";
   for (size_t i = 0; i < h->layers.size(); ++i) {
     const LayerRT& l = h->layers[i];
     for (const auto& kv : l.tuned) {
@@ -1883,7 +1909,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   const int L = (int)h->layers.size();
   std::vector<std::map<int, const tic::ConvEntry*>> tuned(L);
   std::vector<std::map<int, int>> vars(L);
-  int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form, chain = h->chain;
+  int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form, chain = h->chain, chain_wh = h->chain_wh;
   const char* p = text;
   int line = 0;
   while (*p) {
@@ -1904,6 +1930,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
       else if (!strcmp(name, "s1_form") && (a == 0 || a == 1)) s1_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
+      else if (!strcmp(name, "chain_wh") && (a == 1 || a == 2)) chain_wh = a;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
     } else if (!strcmp(kind, "conv")) {
       if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)
@@ -1938,6 +1965,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   h->fuse_tail = fuse_tail;
   h->s1_form = s1_form;
   h->chain = chain;
+  h->chain_wh = chain_wh;
   return TIC_OK;
 }
 

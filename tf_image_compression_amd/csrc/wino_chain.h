@@ -91,13 +91,19 @@ __device__ __forceinline__ f32x4 ld_sc1(const float* p) {
 }  // namespace chain
 
 // IN: IN_F32 / IN_IDX for the first layer; OUT: OUT_F32 / OUT_QUANT for the last one.
-template <int IN, int OUT>
-__global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
+// WH: waves per transform-point row — 1: a 256-thread workgroup, wave xi computes all 64
+// output channels of points (xi, 0..3); 2: a 512-thread workgroup, waves xi and xi + 4
+// split the output channels in halves (two waves per SIMD hide each other's LDS / L2
+// latency; every output's fma order is unchanged, so both are bit-identical).
+template <int IN, int OUT, int WH = 1>
+__global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(const ChainArgs a) {
   using namespace chain;
+  constexpr int NTH = 256 * WH;
   __shared__ __attribute__((aligned(16))) float smem[2 * TB];
   __shared__ unsigned sh[2];
   const int tid = threadIdx.x;
-  const int xi = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int xi = wv & 3, wh = wv >> 2;  // point row, output-channel part
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
   const int H = a.H, W = a.W, R = a.rh * a.rw, nR = a.n * R;
 
@@ -113,12 +119,12 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
   const int oy0 = ry * 8, ox0 = rx * 8;
 
   // ---- weights of layer l, step s = 4 kc + nu, straight from L2, prefetched PF ahead ----
-  constexpr int NSTEP = 4 * KC, PF = 3, NBW = 4;
+  constexpr int NSTEP = 4 * KC, PF = 3, NBW = 4 / WH;
   f32x4 av[PF + 1][NBW];
   auto wglob = [&](int l, int s, int nb) -> f32x4 {
     const int kc = s >> 2, nu = s & 3;
     const float* wl = a.layer[l].wu + (size_t)xi * 64 * KC * C + (size_t)(lg * C + li) * 4;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * C + nb * 64);
+    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * C + (wh * NBW + nb) * 64);
   };
 #pragma unroll
   for (int p = 0; p < PF; ++p)
@@ -132,11 +138,11 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
   float* src = first_block ? smem : smem + TB;
   {
     constexpr int NSTAGE = LR * 10 * (C / 4);  // 1600 16-byte chunks
-    constexpr int NIT = (NSTAGE + 255) / 256;
+    constexpr int NIT = (NSTAGE + NTH - 1) / NTH;
     f32x4 tmp[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int e = i * 256 + tid;
+      const int e = i * NTH + tid;
       tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (e < NSTAGE) {
         const int c4 = e % 16, pe = e / 16, col = pe % 10, row = pe / 10;
@@ -157,7 +163,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int e = i * 256 + tid;
+      const int e = i * NTH + tid;
       if (e < NSTAGE) {
         const int c4 = e % 16, pe = e / 16, col = pe % 10, row = pe / 10;
         *reinterpret_cast<f32x4*>(&src[tpix(row, col) + c4 * 4]) = tmp[i];
@@ -172,8 +178,11 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
   const int ty_l = li / TTX, tx_l = li % TTX;
   const int offA = ((2 * ty_l + iA) * RP + tx_l) * PS + lg * 4;
   const int offB = ((2 * ty_l + iB) * RP + tx_l) * PS + lg * 4;
-  // epilogue ownership: one (tile, channel quad) per thread
-  const int et = tid >> 4, eq = tid & 15;
+  // epilogue ownership: one (tile, channel quad) per thread and output row ay (WH = 2:
+  // the threads tid and tid + 256 take the tile's rows 0 and 1)
+  const int et = (tid & 255) >> 4, eq = tid & 15;
+  const int ay0 = WH == 1 ? 0 : tid >> 8;
+  constexpr int nay = WH == 1 ? 2 : 1;
   const int ety = et / TTX, etx = et % TTX;
   bool failed = false;
 
@@ -248,27 +257,28 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const f32x4 m0 = acc[0][nb], m1 = acc[1][nb], m2 = acc[2][nb], m3 = acc[3][nb];
-      float* x = &xch[(xi * 2 * NT + li) * XS + nb * 16 + lg * 4];
+      float* x = &xch[(xi * 2 * NT + li) * XS + (wh * NBW + nb) * 16 + lg * 4];
       *reinterpret_cast<f32x4*>(x) = (m0 + m1) + m2;
       *reinterpret_cast<f32x4*>(x + NT * XS) = (m1 - m2) - m3;
     }
     __syncthreads();
 
     // ---- Y = A^T T for (tile et, quad eq), + bias, act, + residual ----
-    f32x4 T[4][2];
-#pragma unroll
-    for (int x2 = 0; x2 < 4; ++x2)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) T[x2][b] = *reinterpret_cast<const f32x4*>(&xch[((x2 * 2 + b) * NT + et) * XS + 4 * eq]);
+    // row ay of Y from T rows ay..ay+2: (T0 + T1) + T2, or (T1 - T2) - T3
     const int co = 4 * eq;
     const f32x4 bb = *reinterpret_cast<const f32x4*>(a.layer[l].bias + co);
     const bool relu = a.layer[l].act == ACT_RELU;
-    f32x4 y[2][2];
+    f32x4 y[2][2];  // [k][b], output row ay0 + k
 #pragma unroll
-    for (int ay = 0; ay < 2; ++ay)
+    for (int k = 0; k < nay; ++k) {
+      const int ay = ay0 + k;
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        f32x4 v = ay == 0 ? (T[0][b] + T[1][b]) + T[2][b] : (T[1][b] - T[2][b]) - T[3][b];
+        f32x4 t[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          t[j] = *reinterpret_cast<const f32x4*>(&xch[(((ay + j) * 2 + b) * NT + et) * XS + 4 * eq]);
+        f32x4 v = ay == 0 ? (t[0] + t[1]) + t[2] : (t[0] - t[1]) - t[2];
         v.x = __fadd_rn(v.x, bb.x);
         v.y = __fadd_rn(v.y, bb.y);
         v.z = __fadd_rn(v.z, bb.z);
@@ -286,18 +296,19 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
           v.z = __fadd_rn(v.z, rr.z);
           v.w = __fadd_rn(v.w, rr.w);
         }
-        y[ay][b] = v;
+        y[k][b] = v;
       }
+    }
 
     if (last) {  // ---- the chain's output: global f32 or the quantiser ----
 #pragma unroll
-      for (int ay = 0; ay < 2; ++ay)
+      for (int k = 0; k < nay; ++k)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-          const int oy = oy0 + 2 * ety + ay, ox = ox0 + 2 * etx + b;
+          const int oy = oy0 + 2 * ety + ay0 + k, ox = ox0 + 2 * etx + b;
           if (oy >= H || ox >= W) continue;
           const size_t o = ((size_t)(nimg * H + oy) * W + ox) * C + co;
-          const f32x4 v = y[ay][b];
+          const f32x4 v = y[k][b];
           if constexpr (OUT == OUT_F32) {
             *reinterpret_cast<f32x4*>(a.out + o) = v;
           } else {
@@ -313,12 +324,12 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
     // ---- into the next layer's tile (interior), zero outside the image ----
     if (xch == dst) __syncthreads();  // every thread has read its T from dst's space
 #pragma unroll
-    for (int ay = 0; ay < 2; ++ay)
+    for (int k = 0; k < nay; ++k)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const int ly = 2 * ety + ay, lx = 2 * etx + b;
+        const int ly = 2 * ety + ay0 + k, lx = 2 * etx + b;
         const bool in_img = oy0 + ly < H && ox0 + lx < W;
-        *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[ay][b] : f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[k][b] : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     __syncthreads();
 
@@ -327,8 +338,8 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
       const size_t g = (size_t)nimg * R + reg;
       float* const xb = a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C);
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {  // 4 sides x 8 pixels x 16 quads = 512 chunks
-        const int e = k * 256 + tid;
+      for (int k = 0; k < 512 / NTH; ++k) {  // 4 sides x 8 pixels x 16 quads = 512 chunks
+        const int e = k * NTH + tid;
         const int side = e >> 7, px = (e >> 4) & 7, q = e & 15;
         const int ly = side == 0 ? 0 : (side == 1 ? 7 : px), lx = side == 2 ? 0 : (side == 3 ? 7 : px);
         st_sc1(xb + (side * 8 + px) * C + 4 * q, *reinterpret_cast<const f32x4*>(&dst[tpix(ly + 1, lx + 1) + 4 * q]));
@@ -353,7 +364,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
       }
       __syncthreads();
       // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16 quads
-      for (int e = tid; e < 36 * 16; e += 256) {
+      for (int e = tid; e < 36 * 16; e += NTH) {
         const int hp = e >> 4, q = e & 15;
         int hy, hx;
         if (hp < 10) hy = -1, hx = hp - 1;
@@ -378,7 +389,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_kernel(const ChainArgs a) {
       __syncthreads();
     } else {
       // a single region per patch: the halo is all outside the image
-      for (int e = tid; e < 36 * 16; e += 256) {
+      for (int e = tid; e < 36 * 16; e += NTH) {
         const int hp = e >> 4, q = e & 15;
         int hy, hx;
         if (hp < 10) hy = -1, hx = hp - 1;

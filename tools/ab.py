@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--cfg", action="append", required=True, help="k=v[,k=v] codec options; env:KEY=V for env")
+    ap.add_argument("--tune-file", default=None, help="replay this tools/tune/*.json state instead of tuning")
+    ap.add_argument("--refork", action="store_true", help="every round starts from a fresh fork of the lanes")
     args = ap.parse_args()
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
@@ -45,7 +47,10 @@ def main():
             else:
                 codec.set_option(k, int(v))
 
-    for cfg in args.cfg:  # autotune each configuration's lane batch once
+    if args.tune_file:
+        with open(args.tune_file) as f:
+            codec.tuning_import(json.load(f)["tuning"])
+    for cfg in args.cfg:  # autotune each configuration's lane batch once (no-op where replayed)
         apply(cfg)
         m = [int(kv.split("=")[1]) for kv in cfg.split(",") if kv.startswith("streams=")]
         k = m[-1] if m else 2
@@ -55,6 +60,9 @@ def main():
     for r in range(args.rounds):
         for cfg in args.cfg:
             apply(cfg)
+            if args.refork:
+                codec.synchronize()
+                codec.set_option("decouple", 1)  # marks the handle stream dirty: the next call forks
             for _ in range(3):
                 codec.codec_device(d_in, B, d_idx, d_rgb)
             codec.synchronize()
@@ -64,7 +72,8 @@ def main():
             codec.synchronize()
             res[cfg].append((time.perf_counter() - t0) * 1e3 / args.steps)
     out = {c: {"median_ms": round(statistics.median(v), 4), "min_ms": round(min(v), 4),
-               "mpix_s": round(B * P * P / statistics.median(v) / 1e3, 1)} for c, v in res.items()}
+               "mpix_s": round(B * P * P / statistics.median(v) / 1e3, 1),
+               "rounds_ms": [round(x, 4) for x in v]} for c, v in res.items()}
     print(json.dumps(out, indent=1))
 
 
