@@ -353,6 +353,10 @@ struct Lane {
   unsigned* cflags = nullptr;
   size_t cflags_n = 0;
   unsigned* ctl = nullptr;
+  // TIC_CHAIN_TIMING: per chain launch slot (0 encoder side / rmbe, 1 decoder side) the
+  // phase timestamps of the last launch, [grid][CH_TS]
+  unsigned long long* tstamp[2] = {nullptr, nullptr};
+  int tstamp_grid[2] = {0, 0};
 };
 
 struct tic_handle {
@@ -487,6 +491,21 @@ int ensure_chain(tic_handle* h, Lane& ln, int nl, int n, int R) {
 // A chain hand-off that timed out (wino_chain_kernel's bounded poll) leaves an error word;
 // report it (and clear it) at the next synchronisation point.
 int check_chain_error(tic_handle* h) {
+  if (const char* path = getenv("TIC_CHAIN_TIMING")) {  // append {lane, slot, grid, CH_TS} + stamps
+    if (FILE* f = fopen(path, "ab")) {
+      for (int li = 0; li < 4; ++li)
+        for (int slot = 0; slot < 2; ++slot) {
+          const Lane& ln = h->lanes[li];
+          if (!ln.tstamp[slot]) continue;
+          std::vector<unsigned long long> t((size_t)ln.tstamp_grid[slot] * tic::CH_TS);
+          if (hipMemcpy(t.data(), ln.tstamp[slot], t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) break;
+          const int hdr[4] = {li, slot, ln.tstamp_grid[slot], tic::CH_TS};
+          fwrite(hdr, sizeof hdr, 1, f);
+          fwrite(t.data(), 8, t.size(), f);
+        }
+      fclose(f);
+    }
+  }
   for (Lane& ln : h->lanes) {
     if (!ln.ctl) continue;
     unsigned w[4] = {0, 0, 0, 0};
@@ -764,6 +783,18 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.flags = ln.cflags;
       a.ctl = ln.ctl;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
+      if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
+        const int slot = first_dec ? 1 : 0, grid = n * R;
+        if (ln.tstamp_grid[slot] < grid) {
+          if (ln.tstamp[slot]) (void)hipFree(ln.tstamp[slot]);
+          ln.tstamp[slot] = nullptr;
+          ln.tstamp_grid[slot] = 0;
+          HIP_TRY(hipMalloc((void**)&ln.tstamp[slot], (size_t)grid * tic::CH_TS * sizeof(unsigned long long)));
+          HIP_TRY(hipMemsetAsync(ln.tstamp[slot], 0, (size_t)grid * tic::CH_TS * sizeof(unsigned long long), st));
+          ln.tstamp_grid[slot] = grid;
+        }
+        a.tstamp = ln.tstamp[slot];
+      }
       if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
                                   st, h->chain_wh))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);
@@ -1128,6 +1159,8 @@ void tic_destroy(tic_handle* h) {
     if (ln.xbuf) (void)hipFree(ln.xbuf);
     if (ln.cflags) (void)hipFree(ln.cflags);
     if (ln.ctl) (void)hipFree(ln.ctl);
+    for (auto* t : ln.tstamp)
+      if (t) (void)hipFree(t);
   }
   for (int i = 0; i < 4; ++i) {
     if (h->lanes[i].stream) {

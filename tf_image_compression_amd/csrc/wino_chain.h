@@ -34,6 +34,9 @@
 namespace tic {
 
 constexpr int CH_MAX_LAYERS = 8;
+// timestamps per workgroup: kernel start, input staged, then per layer: start, K loop done,
+// epilogue done, border published, neighbours' flags seen, halo staged
+constexpr int CH_TS = 2 + 6 * CH_MAX_LAYERS;
 
 struct ChainLayer {
   const float* wu;    // Winograd U [16 p][4 kc][4 g][64][4 t] (pack_wino)
@@ -58,6 +61,8 @@ struct ChainArgs {
   unsigned* ctl;        // [0] ticket, [1] done count, [2] epoch, [3] error (poll timeout)
   int probe;            // timing probes only (TIC_CHAIN_PROBE; results invalid unless 0):
                         // 1 = no hand-off at all, 2 = publish but do not wait / read
+  unsigned long long* tstamp;  // phase timestamps (TIC_CHAIN_TIMING; results stay valid) or
+                               // null: [workgroup][CH_TS] s_memrealtime (100 MHz) by thread 0
 };
 
 namespace chain {
@@ -99,18 +104,29 @@ template <int IN, int OUT, int WH = 1>
 __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(const ChainArgs a) {
   using namespace chain;
   constexpr int NTH = 256 * WH;
-  __shared__ __attribute__((aligned(16))) float smem[2 * TB];
+  // WH = 2 (one workgroup per CU): the T exchange gets a buffer of its own beside the two
+  // tiles, so it never aliases a tile and needs no barrier of its own
+  constexpr bool SEPX = WH == 2;
+  constexpr int TSTR = SEPX ? TILE : TB;
+  __shared__ __attribute__((aligned(16))) float smem[SEPX ? 2 * TILE + XCH : 2 * TB];
+  __shared__ __attribute__((aligned(16))) float sbias[CH_MAX_LAYERS * C];
   __shared__ unsigned sh[2];
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int xi = wv & 3, wh = wv >> 2;  // point row, output-channel part
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
   const int H = a.H, W = a.W, R = a.rh * a.rw, nR = a.n * R;
+  auto stamp = [&](int k) {
+    if (a.tstamp && tid == 0) a.tstamp[(size_t)blockIdx.x * CH_TS + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   if (tid == 0) {
     sh[0] = __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh[1] = __hip_atomic_load(&a.ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // every layer's bias, read by the epilogues from LDS
+  for (int e = tid; e < a.nl * C; e += NTH) sbias[e] = a.layer[e / C].bias[e % C];
   __syncthreads();
   const int ticket = (int)sh[0];
   const unsigned epoch = sh[1] + 1u;  // this launch's flag value
@@ -135,7 +151,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   // The first layer's tile is the res_block input when the chain starts a block, so it
   // goes to tile 0 (A) then, else to tile 1 (B): the block input always lives in A.
   const bool first_block = a.nl > 1 && a.layer[1].res;
-  float* src = first_block ? smem : smem + TB;
+  float* src = first_block ? smem : smem + TSTR;
   {
     constexpr int NSTAGE = LR * 10 * (C / 4);  // 1600 16-byte chunks
     constexpr int NIT = (NSTAGE + NTH - 1) / NTH;
@@ -171,6 +187,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     }
   }
   __syncthreads();
+  stamp(1);
 
   // B^T row xi from input rows iA, iB of each tile (conv3x3_wino_kernel's exact signs)
   const int iA = xi == 0 ? 0 : 1, iB = xi == 3 ? 3 : 2;
@@ -190,9 +207,11 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     const bool last = l == a.nl - 1;
     const bool res = a.layer[l].res != 0;
     const bool starts_block = !last && a.layer[l + 1].res != 0;
-    float* const dst = src == smem ? smem + TB : smem;  // the other tile
-    float* const xch = starts_block ? dst : src;        // T exchange: never the block input
+    float* const dst = src == smem ? smem + TSTR : smem;  // the other tile
+    float* const xch = SEPX ? smem + 2 * TILE : starts_block ? dst : src;  // T exchange: never the block input
     float* const rsd = dst;                              // res layers: the block input tile
+    const int ts = 2 + 6 * l;
+    stamp(ts);
 
     // ---- K loop: conv3x3_wino_kernel's order ----
     f32x4 d[2][4];
@@ -252,8 +271,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(l + 1, p, nb);
     }
 
+    stamp(ts + 1);
     // ---- T = M A over nu, exchanged through LDS ----
-    __syncthreads();  // every wave is done reading src (xch may alias it)
+    if (!SEPX) __syncthreads();  // every wave is done reading src (xch may alias it)
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const f32x4 m0 = acc[0][nb], m1 = acc[1][nb], m2 = acc[2][nb], m3 = acc[3][nb];
@@ -266,7 +286,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     // ---- Y = A^T T for (tile et, quad eq), + bias, act, + residual ----
     // row ay of Y from T rows ay..ay+2: (T0 + T1) + T2, or (T1 - T2) - T3
     const int co = 4 * eq;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(a.layer[l].bias + co);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(&sbias[l * C + co]);
     const bool relu = a.layer[l].act == ACT_RELU;
     f32x4 y[2][2];  // [k][b], output row ay0 + k
 #pragma unroll
@@ -318,6 +338,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
             *reinterpret_cast<uint32_t*>(a.qout + o) = q;
           }
         }
+      stamp(ts + 2);
       break;
     }
 
@@ -332,6 +353,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[k][b] : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     __syncthreads();
+    stamp(ts + 2);
 
     // ---- hand-off: publish this region's border, then read the neighbours' ----
     if (R > 1 && a.probe != 1) {
@@ -347,6 +369,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(&a.flags[(size_t)l * nR + g], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      stamp(ts + 3);
       // wait for the (up to 8) neighbours' flags of this layer
       if (a.probe == 0 && tid < 9 && tid != 4) {
         const int nry = ry + tid / 3 - 1, nrx = rx + tid % 3 - 1;
@@ -363,6 +386,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         }
       }
       __syncthreads();
+      stamp(ts + 4);
       // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16 quads
       for (int e = tid; e < 36 * 16; e += NTH) {
         const int hp = e >> 4, q = e & 15;
@@ -387,6 +411,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         *reinterpret_cast<f32x4*>(&dst[tpix(hy + 1, hx + 1) + 4 * q]) = v;
       }
       __syncthreads();
+      stamp(ts + 5);
     } else {
       // a single region per patch: the halo is all outside the image
       for (int e = tid; e < 36 * 16; e += NTH) {

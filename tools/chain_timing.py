@@ -1,0 +1,92 @@
+"""Where wino_chain_kernel's time goes, phase by phase, inside the two-lane step.
+
+Runs the bench's configuration (model_0, 256^2, batch 64, the committed tuning replayed)
+with TIC_CHAIN_TIMING set: every chain launch records s_memrealtime (100 MHz) at its
+phase boundaries (wino_chain.h, CH_TS), and tic_synchronize appends the last launch's
+stamps to a file.  Prints, per chain launch (lane, encoder/decoder side), the spread of
+workgroup start times and the median / 90th-percentile duration of every phase per layer.
+
+    python tools/chain_timing.py [--tune-file tools/tune/model0_p256_b64_s2.json] [--steps 20]
+"""
+import argparse
+import json
+import os
+import struct
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PHASES = ["mfma", "epilogue", "publish", "wait", "halo"]
+
+
+def read_dumps(path):
+    out = []
+    with open(path, "rb") as f:
+        while True:
+            h = f.read(16)
+            if len(h) < 16:
+                break
+            lane, slot, grid, ts = struct.unpack("4i", h)
+            t = np.frombuffer(f.read(8 * grid * ts), dtype=np.uint64).reshape(grid, ts)
+            out.append((lane, slot, t))
+    return out
+
+
+def summarise(t, nl):
+    us = lambda a: a.astype(np.float64) / 100.0  # 100 MHz ticks -> us
+    t = t.astype(np.int64)
+    start = t[:, 0]
+    rep = {"workgroups": int(t.shape[0]),
+           "start_spread_us": round(float(us(start.max() - start.min())), 2),
+           "stage_us": round(float(np.median(us(t[:, 1] - t[:, 0]))), 2),
+           "kernel_us": round(float(us(t[:, 2 + 6 * (nl - 1) + 2].max() - start.min())), 2),
+           "layers": []}
+    for l in range(nl):
+        b = 2 + 6 * l
+        row = {}
+        marks = [b, b + 1, b + 2] + ([b + 3, b + 4, b + 5] if l < nl - 1 else [])
+        for k in range(len(marks) - 1):
+            d = us(t[:, marks[k + 1]] - t[:, marks[k]])
+            row[PHASES[k]] = [round(float(np.median(d)), 2), round(float(np.percentile(d, 90)), 2)]
+        rep["layers"].append(row)
+    return rep
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tune-file", default=os.path.join(ROOT, "tools", "tune", "model0_p256_b64_s2.json"))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--streams", type=int, default=2)
+    args = ap.parse_args()
+    path = os.path.join(tempfile.mkdtemp(), "chain_ts.bin")
+    os.environ["TIC_CHAIN_TIMING"] = path
+    sys.path.insert(0, ROOT)
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import bottleneck_shape
+    P, B, M = 256, 64, 0
+    c = Codec(M, synthetic_params(M, seed=0), SYNTH_MEAN, SYNTH_STD, patch_size=P)
+    c.set_option("streams", args.streams)
+    with open(args.tune_file) as f:
+        c.tuning_import(json.load(f)["tuning"])
+    c.set_option("chain", 1)
+    eh, ew, ec = bottleneck_shape(M, P)
+    x = np.random.default_rng(1234).integers(0, 256, (B, P, P, 3), dtype=np.uint8)
+    d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(B * eh * ew * ec), c.alloc(x.nbytes)
+    d_in.upload(x)
+    for _ in range(args.steps):
+        c.codec_device(d_in, B, d_idx, d_rgb)
+    c.synchronize()  # dumps the last launch of every lane and side
+    dumps = read_dumps(path)
+    nl = 5
+    for lane, slot, t in dumps:
+        rep = summarise(t, nl)
+        rep.update({"lane": lane, "side": "decoder" if slot else "encoder"})
+        print(json.dumps(rep), flush=True)
+    c.close()
+
+
+if __name__ == "__main__":
+    main()
