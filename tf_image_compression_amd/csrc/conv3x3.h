@@ -691,6 +691,13 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
 
   const int tid = threadIdx.x;
   const int gx0 = blockIdx.x * 16, gy0 = blockIdx.y * TH1, nimg = blockIdx.z;
+  // timing probe: s_memrealtime (100 MHz) by thread 0 at the phase boundaries
+  auto stamp = [&](int k) {
+    if (a.tstamp && tid == 0)
+      a.tstamp[((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + k] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
 
@@ -717,29 +724,47 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   };
   // zero the planes first where the tile leaves the image (SAME padding)
   const bool edge = iy0 < 0 || ix0 < 0 || iy0 + R0 > a.H || ix0 + 68 > a.W || !U8 || (ix0 * 3) % 4 != 0;
-  if (edge)
-    for (int e = tid; e < 3 * RGBP; e += 256) rgb[e] = 0.f;
-  if constexpr (U8)
-    for (int e = tid; e < 768; e += 256)
-      lut[e] = __fdiv_rn(__fsub_rn((float)(e & 255), a.mean[e >> 8]), a.std[e >> 8]);
-  if (edge || U8) __syncthreads();
+  // interior u8 tiles: each thread unpacks 4-pixel groups (12 bytes) of the 68-pixel row
+  // segments; their loads are issued first so they fly together with the table's
+  constexpr int GPR = 17, NG = R0 * GPR, NGI = (NG + 255) / 256;
+  uint32_t wpre[NGI][3];
   if constexpr (U8) {
     if (!edge) {
-      // interior: each thread unpacks one 4-pixel group (12 bytes) of a 68-pixel row segment;
+#pragma unroll
+      for (int i = 0; i < NGI; ++i) {
+        const int e = i * 256 + tid;
+        if (e < NG) {
+          const int rr = e / GPR, g = e % GPR;
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(
+              reinterpret_cast<const uint8_t*>(a.in) + ((size_t)(nimg * a.H + iy0 + rr) * a.W + ix0) * 3 + 12 * g);
+          wpre[i][0] = src[0];
+          wpre[i][1] = src[1];
+          wpre[i][2] = src[2];
+        }
+      }
+    }
+  }
+  if (edge)
+    for (int e = tid; e < 3 * RGBP; e += 256) rgb[e] = 0.f;
+  if constexpr (U8)  // the host's f32 table (tic_finalize), same values as (v - mean) / std here
+    for (int e = tid; e < 768; e += 256) lut[e] = a.nlut[e];
+  if (edge || U8) __syncthreads();
+  stamp(1);
+  if constexpr (U8) {
+    if (!edge) {
       // pixel k of group g is column 4g + k: plane k, entry g
-      constexpr int GPR = 17;
-      for (int e = tid; e < R0 * GPR; e += 256) {
+#pragma unroll
+      for (int i = 0; i < NGI; ++i) {
+        const int e = i * 256 + tid;
+        if (e >= NG) break;
         const int rr = e / GPR, g = e % GPR;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(
-            reinterpret_cast<const uint8_t*>(a.in) + ((size_t)(nimg * a.H + iy0 + rr) * a.W + ix0) * 3 + 12 * g);
-        const uint32_t w[3] = {src[0], src[1], src[2]};
         float* const dst = rgb + rr * 4 * QJ + g;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
             const int b = 3 * k + c;
-            dst[c * RGBP + k * QJ] = lut[c * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xff)];
+            dst[c * RGBP + k * QJ] = lut[c * 256 + ((wpre[i][b >> 2] >> (8 * (b & 3))) & 0xff)];
           }
       }
     }
@@ -762,6 +787,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
     }
   }
   __syncthreads();
+  stamp(2);
 
   // ---- layer 0 on every slot of the layer-1 input tile ----
   {
@@ -807,23 +833,33 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
       const int ey = ey0 + r, ex = ex0 + exl;
       return slot < NSLOT && exl < 33 && ey >= 0 && ey < a.H1 && ex >= 0 && ex < a.W1;
     };
+    // branch-free gather of block jb's 7 k-step operands: every lane loads (a slot past the
+    // tile reads slot 0's pixels — its column of the MFMA result is never stored as valid),
+    // then k = 27 (the zero weight row) is zeroed by a select
+    auto gather = [&](int jb, float (&b)[7]) {
+      const int slot = (wave + 4 * jb) * 16 + li;
+      const int r = slot / LC1, cs = slot % LC1;
+      const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
+      const bool rd = slot < NSLOT && 2 * j + plane < 33;
+      const int base = rd ? 2 * r * 4 * QJ + j : 0;
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        const int d = plane ? dl[1][t] : dl[0][t];
+        const float v = rgb[base + (d < 0 ? 0 : d)];
+        b[t] = d >= 0 ? v : 0.f;
+      }
+    };
+    float bq0[2][7];
+    gather(0, bq0[0]);
 #pragma unroll
     for (int jb = 0; jb < NPW; ++jb) {
       const int blk = wave + 4 * jb;
       if (blk >= NBLK0) break;
       const int slot = blk * 16 + li;
-      const int r = slot / LC1, cs = slot % LC1;
-      const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
-      const int exl = 2 * j + plane;  // layer-0 column (local)
-      const int base = 2 * r * 4 * QJ + j;
-      const bool rd = slot < NSLOT && exl < 33;
-      float b[7];
-#pragma unroll
-      for (int t = 0; t < 7; ++t) {
-        const int d = plane ? dl[1][t] : dl[0][t];
-        b[t] = (rd && d >= 0) ? rgb[base + d] : 0.f;
-      }
+      // the next block's operands load under this block's MFMAs
+      if (jb + 1 < NPW) gather(jb + 1, bq0[(jb + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
+      const float(&b)[7] = bq0[jb & 1];
       f32x4 acc[NB0];
 #pragma unroll
       for (int nb = 0; nb < NB0; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -831,6 +867,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
       for (int t = 0; t < 7; ++t)
 #pragma unroll
         for (int nb = 0; nb < NB0; ++nb) acc[nb] = mfma4(t < 4 ? w0[nb][t & 3] : w1[nb][t & 3], b[t], acc[nb]);
+      __builtin_amdgcn_sched_barrier(0);
       // lane holds channels nb*16 + 4 lg .. +3 of slot; relu; zero outside layer 0's image
       if constexpr (CMP) {
 #pragma unroll
@@ -849,6 +886,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
     }
   }
   __syncthreads();
+  stamp(3);
 
   // ---- layer 1: stride-2 implicit GEMM from the LDS tile ----
   f32x4 acc[MB][NB1];
@@ -884,6 +922,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
         for (int nb = 0; nb < NB1; ++nb) acc[mb][nb] = mfma4(av[s % (PF + 1)][nb][t], bq[c][mb][t], acc[mb][nb]);
     __builtin_amdgcn_sched_barrier(0);
   }
+  stamp(4);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int oy = gy0 + wr * MB + mb, ox = gx0 + li;
@@ -900,6 +939,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
       *reinterpret_cast<f32x4*>(a.out + ((size_t)(nimg * a.H2 + oy) * a.W2 + ox) * C1 + co) = v;
     }
   }
+  stamp(5);
 }
 
 }  // namespace tic

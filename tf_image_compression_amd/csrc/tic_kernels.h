@@ -52,6 +52,8 @@ struct Enc01Args {
   int H2, W2;          // layer-1 output size
   int pad0y, pad0x, pad1y, pad1x;  // SAME pad_before of both convs
   float mean[3], std[3];
+  const float* nlut;   // u8 input: [3][256] (v - mean[c]) / std[c] in f32, computed on the host
+  unsigned long long* tstamp;  // phase timestamps (TIC_ENC01_TIMING) or null: [workgroup][8]
 };
 
 struct RgbOutArgs {

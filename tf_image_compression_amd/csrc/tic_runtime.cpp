@@ -353,10 +353,10 @@ struct Lane {
   unsigned* cflags = nullptr;
   size_t cflags_n = 0;
   unsigned* ctl = nullptr;
-  // TIC_CHAIN_TIMING: per chain launch slot (0 encoder side / rmbe, 1 decoder side) the
-  // phase timestamps of the last launch, [grid][CH_TS]
-  unsigned long long* tstamp[2] = {nullptr, nullptr};
-  int tstamp_grid[2] = {0, 0};
+  // timing probes: per slot (0 / 1 the encoder- / decoder-side chain launch, TIC_CHAIN_TIMING;
+  // 2 enc01, TIC_ENC01_TIMING) the phase timestamps of the last launch, [grid][stamps]
+  unsigned long long* tstamp[3] = {nullptr, nullptr, nullptr};
+  int tstamp_grid[3] = {0, 0, 0}, tstamp_n[3] = {tic::CH_TS, tic::CH_TS, 8};
 };
 
 struct tic_handle {
@@ -370,6 +370,7 @@ struct tic_handle {
   float mean[3] = {0, 0, 0}, std[3] = {1, 1, 1};
   bool has_norm = false, finalized = false;
   float* d_lut = nullptr;
+  float* d_nlut = nullptr;  // [3][256] (v - mean[c]) / std[c] in f32 (TF's op order), for u8 input
   int chunk = 256;
   size_t act_elems = 0;  // max f32 activation elements per patch
   // host-entry staging
@@ -490,16 +491,33 @@ int ensure_chain(tic_handle* h, Lane& ln, int nl, int n, int R) {
 
 // A chain hand-off that timed out (wino_chain_kernel's bounded poll) leaves an error word;
 // report it (and clear it) at the next synchronisation point.
+// timing probes: a lane's stamp buffer for `slot`, at least grid x tstamp_n[slot] words
+int probe_stamps(Lane& ln, int slot, int grid, hipStream_t st, unsigned long long** out) {
+  if (ln.tstamp_grid[slot] < grid) {
+    if (ln.tstamp[slot]) (void)hipFree(ln.tstamp[slot]);
+    ln.tstamp[slot] = nullptr;
+    ln.tstamp_grid[slot] = 0;
+    const size_t bytes = (size_t)grid * ln.tstamp_n[slot] * sizeof(unsigned long long);
+    HIP_TRY(hipMalloc((void**)&ln.tstamp[slot], bytes));
+    HIP_TRY(hipMemsetAsync(ln.tstamp[slot], 0, bytes, st));
+    ln.tstamp_grid[slot] = grid;
+  }
+  *out = ln.tstamp[slot];
+  return TIC_OK;
+}
+
 int check_chain_error(tic_handle* h) {
-  if (const char* path = getenv("TIC_CHAIN_TIMING")) {  // append {lane, slot, grid, CH_TS} + stamps
+  const char* path = getenv("TIC_CHAIN_TIMING");
+  if (!path) path = getenv("TIC_ENC01_TIMING");
+  if (path) {  // append {lane, slot, grid, stamps per workgroup} + the stamps
     if (FILE* f = fopen(path, "ab")) {
       for (int li = 0; li < 4; ++li)
-        for (int slot = 0; slot < 2; ++slot) {
+        for (int slot = 0; slot < 3; ++slot) {
           const Lane& ln = h->lanes[li];
           if (!ln.tstamp[slot]) continue;
-          std::vector<unsigned long long> t((size_t)ln.tstamp_grid[slot] * tic::CH_TS);
+          std::vector<unsigned long long> t((size_t)ln.tstamp_grid[slot] * ln.tstamp_n[slot]);
           if (hipMemcpy(t.data(), ln.tstamp[slot], t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) break;
-          const int hdr[4] = {li, slot, ln.tstamp_grid[slot], tic::CH_TS};
+          const int hdr[4] = {li, slot, ln.tstamp_grid[slot], ln.tstamp_n[slot]};
           fwrite(hdr, sizeof hdr, 1, f);
           fwrite(t.data(), 8, t.size(), f);
         }
@@ -692,9 +710,15 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.H2 = a.W2 = l1r.h_out;
       a.pad0y = a.pad0x = same_pad(d.kind, lay.h_in);
       a.pad1y = a.pad1x = same_pad(K_S2, l1r.h_in);
+      a.nlut = h->d_nlut;
       for (int c = 0; c < 3; ++c) {
         a.mean[c] = h->mean[c];
         a.std[c] = h->std[c];
+      }
+      if (getenv("TIC_ENC01_TIMING")) {  // phase timestamps (tools/chain_timing.py --enc01)
+        // sized for the largest grid of any variant (2-row tiles)
+        int rc2 = probe_stamps(ln, 2, n * ((l1r.h_out + 1) / 2) * ((l1r.h_out + 15) / 16), st, &a.tstamp);
+        if (rc2) return rc2;
       }
       auto it = lay.tuned_var.find(-n);  // fused-pair variants keyed by -n
       int var = it != lay.tuned_var.end() ? it->second : tic::kEnc01Default;
@@ -784,16 +808,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.ctl = ln.ctl;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
-        const int slot = first_dec ? 1 : 0, grid = n * R;
-        if (ln.tstamp_grid[slot] < grid) {
-          if (ln.tstamp[slot]) (void)hipFree(ln.tstamp[slot]);
-          ln.tstamp[slot] = nullptr;
-          ln.tstamp_grid[slot] = 0;
-          HIP_TRY(hipMalloc((void**)&ln.tstamp[slot], (size_t)grid * tic::CH_TS * sizeof(unsigned long long)));
-          HIP_TRY(hipMemsetAsync(ln.tstamp[slot], 0, (size_t)grid * tic::CH_TS * sizeof(unsigned long long), st));
-          ln.tstamp_grid[slot] = grid;
-        }
-        a.tstamp = ln.tstamp[slot];
+        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R, st, &a.tstamp);
+        if (rc2) return rc2;
       }
       if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
                                   st, h->chain_wh))
@@ -1171,6 +1187,7 @@ void tic_destroy(tic_handle* h) {
   }
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->d_lut) (void)hipFree(h->d_lut);
+  if (h->d_nlut) (void)hipFree(h->d_nlut);
   if (h->st_in) (void)hipFree(h->st_in);
   if (h->st_out) (void)hipFree(h->st_out);
   if (h->st_out2) (void)hipFree(h->st_out2);
@@ -1282,6 +1299,16 @@ int tic_finalize(tic_handle* h) {
   }
   if (!h->d_lut) HIP_TRY(hipMalloc((void**)&h->d_lut, 256 * sizeof(float)));
   HIP_TRY(hipMemcpy(h->d_lut, lut.data(), 256 * sizeof(float), hipMemcpyHostToDevice));
+  // normalisation of u8 input, (x - mean) / std in float32 as model_0/model.py:44 computes
+  // it (IEEE subtract, then IEEE divide; the kernels' __fsub_rn / __fdiv_rn give the same)
+  std::vector<float> nlut(768);
+  for (int c = 0; c < 3; ++c)
+    for (int v = 0; v < 256; ++v) {
+      const float d = (float)v - h->mean[c];
+      nlut[c * 256 + v] = d / h->std[c];
+    }
+  if (!h->d_nlut) HIP_TRY(hipMalloc((void**)&h->d_nlut, 768 * sizeof(float)));
+  HIP_TRY(hipMemcpy(h->d_nlut, nlut.data(), 768 * sizeof(float), hipMemcpyHostToDevice));
   h->finalized = true;
   return TIC_OK;
 }

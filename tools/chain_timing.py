@@ -1,4 +1,5 @@
-"""Where wino_chain_kernel's time goes, phase by phase, inside the two-lane step.
+"""Where wino_chain_kernel's (or, --enc01, enc01_kernel's) time goes, phase by phase,
+inside the two-lane step.
 
 Runs the bench's configuration (model_0, 256^2, batch 64, the committed tuning replayed)
 with TIC_CHAIN_TIMING set: every chain launch records s_memrealtime (100 MHz) at its
@@ -6,7 +7,7 @@ phase boundaries (wino_chain.h, CH_TS), and tic_synchronize appends the last lau
 stamps to a file.  Prints, per chain launch (lane, encoder/decoder side), the spread of
 workgroup start times and the median / 90th-percentile duration of every phase per layer.
 
-    python tools/chain_timing.py [--tune-file tools/tune/model0_p256_b64_s2.json] [--steps 20]
+    python tools/chain_timing.py [--tune-file tools/tune/model0_p256_b64_s2.json] [--steps 20] [--enc01]
 """
 import argparse
 import json
@@ -54,14 +55,33 @@ def summarise(t, nl):
     return rep
 
 
+ENC01_PHASES = ["lut", "stage", "layer0", "layer1", "store"]
+
+
+def summarise_enc01(t):
+    t = t[t[:, 5] != 0].astype(np.int64)  # workgroups of the launched grid
+    us = lambda a: a.astype(np.float64) / 100.0
+    rep = {"workgroups": int(t.shape[0]),
+           "kernel_us": round(float(us(t[:, 5].max() - t[:, 0].min())), 2),
+           "wg_life_us": [round(float(np.median(us(t[:, 5] - t[:, 0]))), 2),
+                          round(float(np.percentile(us(t[:, 5] - t[:, 0]), 90)), 2)]}
+    for k, name in enumerate(ENC01_PHASES):
+        d = us(t[:, k + 1] - t[:, k])
+        rep[name] = [round(float(np.median(d)), 2), round(float(np.percentile(d, 90)), 2)]
+    # average workgroups alive over the launch
+    rep["mean_alive"] = round(float(np.sum(t[:, 5] - t[:, 0]) / (t[:, 5].max() - t[:, 0].min())), 1)
+    return rep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tune-file", default=os.path.join(ROOT, "tools", "tune", "model0_p256_b64_s2.json"))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--enc01", action="store_true")
     args = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "chain_ts.bin")
-    os.environ["TIC_CHAIN_TIMING"] = path
+    os.environ["TIC_ENC01_TIMING" if args.enc01 else "TIC_CHAIN_TIMING"] = path
     sys.path.insert(0, ROOT)
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
@@ -71,7 +91,8 @@ def main():
     c.set_option("streams", args.streams)
     with open(args.tune_file) as f:
         c.tuning_import(json.load(f)["tuning"])
-    c.set_option("chain", 1)
+    if not args.enc01:
+        c.set_option("chain", 1)
     eh, ew, ec = bottleneck_shape(M, P)
     x = np.random.default_rng(1234).integers(0, 256, (B, P, P, 3), dtype=np.uint8)
     d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(B * eh * ew * ec), c.alloc(x.nbytes)
@@ -82,6 +103,11 @@ def main():
     dumps = read_dumps(path)
     nl = 5
     for lane, slot, t in dumps:
+        if slot == 2:
+            rep = summarise_enc01(t)
+            rep.update({"lane": lane, "kernel": "enc01"})
+            print(json.dumps(rep), flush=True)
+            continue
         rep = summarise(t, nl)
         rep.update({"lane": lane, "side": "decoder" if slot else "encoder"})
         print(json.dumps(rep), flush=True)
