@@ -665,8 +665,6 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   constexpr int LR1 = 2 * TH1 + 1, LC1 = 34, PS1 = CMP ? C0 : C0 + 8;
   constexpr int NCH = C0 / 4, GRP = 16 / NCH;  // CMP swizzle: chunks per slot, slots per 256 B
   constexpr int T1 = LR1 * LC1 * PS1;    // layer-1 input tile (floats)
-  constexpr int NSLOT = LR1 * LC1;
-  constexpr int NBLK0 = (NSLOT + 15) / 16;
   constexpr int NB0 = C0 / 16;
   constexpr int KC1 = C0 / 16;
   constexpr int WR = TH1 >= 4 ? 4 : 2;   // waves split rows x channel blocks for layer 1
@@ -813,8 +811,13 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
         dl[pl][t] = k < 27 ? c * RGBP + ky * 4 * QJ + (q & 3) * QJ + (q >> 2) : -1;
       }
     }
-    constexpr int NPW = (NBLK0 + 3) / 4;  // blocks per wave
-    f32x4 res[CMP ? NPW : 1][NB0];         // CMP: layer-0 results held until the RGB planes are dead
+    // Blocks of 16 slots: block 2r + p = tile row r, column plane p, j = 0..15 — a wave's
+    // blocks (wave + 4 jb) all have the plane of its own parity; blocks 2 LR1 + q = plane 0's
+    // j = 16 of rows 16 q + li.  Plane 1's j = 16 (layer-0 column 33) is never read by
+    // layer 1 and is not computed.
+    constexpr int NBL = 2 * LR1 + (LR1 + 15) / 16;
+    constexpr int NPW = (NBL + 3) / 4;  // blocks per wave
+    f32x4 res[CMP ? NPW : 1][NB0];       // CMP: layer-0 results held until the RGB planes are dead
     auto put0 = [&](int slot, bool valid, const f32x4 (&acc)[NB0]) {
 #pragma unroll
       for (int nb = 0; nb < NB0; ++nb) {
@@ -826,36 +829,49 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
         *reinterpret_cast<f32x4*>(&t1[t1c(slot, nb * 4 + lg)]) = v;
       }
     };
-    auto slot_valid = [&](int slot) {
-      const int r = slot / LC1, cs = slot % LC1;
-      const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
-      const int exl = 2 * j + plane;
-      const int ey = ey0 + r, ex = ex0 + exl;
-      return slot < NSLOT && exl < 33 && ey >= 0 && ey < a.H1 && ex >= 0 && ex < a.W1;
+    // lane li's slot in block blk, whether the block holds it, and whether it lies inside
+    // layer 0's image (else it is layer 1's zero padding)
+    auto lo_row = [&](int blk) { return (blk - 2 * LR1) * 16 + li; };  // leftover blocks' row
+    auto blk_slot = [&](int blk) {
+      return blk < 2 * LR1 ? (blk >> 1) * LC1 + (blk & 1) * 17 + li : lo_row(blk) * LC1 + 16;
     };
-    // branch-free gather of block jb's 7 k-step operands: every lane loads (a slot past the
-    // tile reads slot 0's pixels — its column of the MFMA result is never stored as valid),
-    // then k = 27 (the zero weight row) is zeroed by a select
-    auto gather = [&](int jb, float (&b)[7]) {
-      const int slot = (wave + 4 * jb) * 16 + li;
-      const int r = slot / LC1, cs = slot % LC1;
-      const int plane = cs >= 17 ? 1 : 0, j = cs - 17 * plane;
-      const bool rd = slot < NSLOT && 2 * j + plane < 33;
-      const int base = rd ? 2 * r * 4 * QJ + j : 0;
+    auto blk_has = [&](int blk) { return blk < 2 * LR1 || (blk < NBL && lo_row(blk) < LR1); };
+    const bool inner0 = ey0 >= 0 && ey0 + LR1 <= a.H1 && ex0 >= 0 && ex0 + 33 <= a.W1;  // tile inside layer 0
+    auto blk_valid = [&](int blk) {
+      if (inner0) return true;
+      const int r = blk < 2 * LR1 ? blk >> 1 : lo_row(blk);
+      const int exl = blk < 2 * LR1 ? 2 * li + (blk & 1) : 32;
+      const int ey = ey0 + r, ex = ex0 + exl;
+      return exl < 33 && ey >= 0 && ey < a.H1 && ex >= 0 && ex < a.W1;
+    };
+    // the 7 k-step offsets of this wave's plane and of plane 0 (k = 27, the zero weight row,
+    // reads offset 0 and is zeroed below)
+    int dw[7], dz[7];
 #pragma unroll
-      for (int t = 0; t < 7; ++t) {
-        const int d = plane ? dl[1][t] : dl[0][t];
-        const float v = rgb[base + (d < 0 ? 0 : d)];
-        b[t] = d >= 0 ? v : 0.f;
+    for (int t = 0; t < 7; ++t) {
+      const int d = (wave & 1) ? dl[1][t] : dl[0][t];
+      dw[t] = d < 0 ? 0 : d;
+      dz[t] = dl[0][t] < 0 ? 0 : dl[0][t];
+    }
+    auto gather = [&](int jb, float (&b)[7]) {
+      const int blk = wave + 4 * jb;
+      if (blk < 2 * LR1) {  // wave-uniform
+        const int base = (blk >> 1) * 8 * QJ + li;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) b[t] = rgb[base + dw[t]];
+      } else {
+        const int base = (lo_row(blk) < LR1 ? lo_row(blk) : 0) * 8 * QJ + 16;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) b[t] = rgb[base + dz[t]];
       }
+      if (lg == 3) b[6] = 0.f;  // k = 27
     };
     float bq0[2][7];
     gather(0, bq0[0]);
 #pragma unroll
     for (int jb = 0; jb < NPW; ++jb) {
       const int blk = wave + 4 * jb;
-      if (blk >= NBLK0) break;
-      const int slot = blk * 16 + li;
+      if (blk >= NBL) break;
       // the next block's operands load under this block's MFMAs
       if (jb + 1 < NPW) gather(jb + 1, bq0[(jb + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
@@ -868,20 +884,20 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
 #pragma unroll
         for (int nb = 0; nb < NB0; ++nb) acc[nb] = mfma4(t < 4 ? w0[nb][t & 3] : w1[nb][t & 3], b[t], acc[nb]);
       __builtin_amdgcn_sched_barrier(0);
-      // lane holds channels nb*16 + 4 lg .. +3 of slot; relu; zero outside layer 0's image
+      // lane holds channels nb*16 + 4 lg .. +3 of its slot; relu; zero outside layer 0's image
       if constexpr (CMP) {
 #pragma unroll
         for (int nb = 0; nb < NB0; ++nb) res[jb][nb] = acc[nb];
-      } else if (slot < NSLOT) {
-        put0(slot, slot_valid(slot), acc);
+      } else if (blk_has(blk)) {
+        put0(blk_slot(blk), blk_valid(blk), acc);
       }
     }
     if constexpr (CMP) {
       __syncthreads();  // every wave is done with the RGB planes the tile overwrites
 #pragma unroll
       for (int jb = 0; jb < NPW; ++jb) {
-        const int blk = wave + 4 * jb, slot = blk * 16 + li;
-        if (blk < NBLK0 && slot < NSLOT) put0(slot, slot_valid(slot), res[jb]);
+        const int blk = wave + 4 * jb;
+        if (blk < NBL && blk_has(blk)) put0(blk_slot(blk), blk_valid(blk), res[jb]);
       }
     }
   }
