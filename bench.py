@@ -81,17 +81,33 @@ def parse():
 def kernel_groups(codec, model_id, P, ms, kernels=None):
     """Group layers by the kernel instance they launch (same template args + shape).  A
     layer whose kernel name is '' ran inside the previous layer's launch (enc01_kernel,
-    dec10_kernel): the pair is one group, its work the sum of both minus the intermediate
-    activation that never reaches HBM (written and read once in the unfused form)."""
+    dec10_kernel: a pair; wino_chain_kernel: a run of stride-1 layers): the launch is one
+    group, its work the sum of its layers and its HBM bytes the first layer's input plus the
+    last layer's output (the intermediate activations and residual inputs stay on chip).
+    A layer inside a Winograd launch counts the Winograd form's FLOPs."""
     from tf_image_compression_amd.topology import layer_work, RMBE_ID, weight_bytes
     work = layer_work(model_id, P)
     L = len(work)
     n_enc = sum(1 for lay, *_ in work if lay.stage == "enc")
     groups = {}
     rows = []
-    if kernels is not None:  # Winograd-form layers: count the FLOPs of the form that runs
-        work = [(lay, f * WINO_FRAC if "wino" in kernels[i] else f, b, ho)
+    if kernels is not None:  # the kernel each layer runs in ('' = the launch before it)
+        launch = []
+        for k in kernels:
+            launch.append(k if k or not launch else launch[-1])
+        work = [(lay, f * WINO_FRAC if "wino" in launch[i] else f, b, ho)
                 for i, (lay, f, b, ho) in enumerate(work)]
+
+    def out_res_bytes(i):
+        lay, _, _, ho = work[i]
+        if model_id != RMBE_ID and i == n_enc - 1:
+            out_b = ho * ho * lay.cout  # u8 symbols
+        elif i == L - 1:
+            out_b = ho * ho * 3 * (4 if model_id == RMBE_ID else 1)
+        else:
+            out_b = ho * ho * lay.cout * 4
+        return out_b, (ho * ho * lay.cout * 4 if lay.residual else 0)
+
     for i, (lay, flops, nbytes, ho) in enumerate(work):
         role = "rgb_in" if i == 0 else ("rgb_out" if i == L - 1 else
                                         ("quant" if (model_id != RMBE_ID and i == n_enc - 1) else
@@ -106,20 +122,24 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
         r = rows[i]
         key, names = tuple(r["key"]), [lay.name]
         f, b, wb, t = flops, nbytes, weight_bytes(lay), float(ms[i])
-        if kernels is not None and i + 1 < L and kernels[i + 1] == "":
-            nl, nf, nb_, nho = work[i + 1]
+        j = i
+        while kernels is not None and j + 1 < L and kernels[j + 1] == "":
+            j += 1
+            nl, nf, _, _ = work[j]
             f += nf
-            b += nb_ - 2 * ho * ho * lay.cout * 4  # the f32 intermediate stays on chip
             wb += weight_bytes(nl)
-            t += float(ms[i + 1])
+            t += float(ms[j])
             names.append(nl.name)
             key = key + ("fused", nl.name)
-            i += 1
+        if j > i:  # first layer's input + last layer's output
+            o_i, r_i = out_res_bytes(i)
+            o_j, _ = out_res_bytes(j)
+            b = (nbytes - o_i - r_i) + o_j
         g = groups.setdefault(key, {"layers": [], "ms": 0.0, "flops": f, "bytes": b, "wbytes": wb, "launches": 0})
         g["layers"].extend(names)
         g["ms"] += t
         g["launches"] += 1
-        i += 1
+        i = j + 1
     return groups, rows
 
 
@@ -376,6 +396,12 @@ def main():
     roof["kernel"] = "+".join(groups[dom_key]["layers"])
     roof["kernel_instance"] = dom_kernels
     roof["ms_per_launch"] = round(dom_ms, 5)
+    # every launch group's roofline, largest time first (the dominant one is `roofline`)
+    roof_groups = []
+    for k in sorted(groups, key=lambda k: -groups[k]["ms"]):
+        rg, rms, _, _ = roofline_of(groups[k], lane_b)
+        roof_groups.append({"kernel": "+".join(groups[k]["layers"]), "launches": groups[k]["launches"],
+                            "ms_per_launch": round(rms, 5), "bound": rg["bound"], "frac": rg["frac"]})
 
     step_ms = t_max * 1e3 / args.steps
     total_px = world * B * P * P * args.steps
@@ -397,6 +423,7 @@ def main():
                    "model": f"model_{M}", "global_batch": B * world, "patch": P,
                    "code_shape": [eh, ew, ec], "parallelism": f"image-parallel x{world}"},
         "roofline": roof,
+        "roofline_groups": roof_groups,
         "roofline_step_frac": round(step_roofline(rows, B, step_ms), 4),
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "hip_graph": bool(args.graph)},
         "tuning": tuning,

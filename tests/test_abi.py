@@ -164,3 +164,36 @@ def test_bench_groups_fused_layer_pairs():
     assert fused[0]["flops"] == f1 + f0
     assert fused[0]["bytes"] == b1 + b0 - 2 * ho1 * ho1 * l1.cout * 4 == 64 * 64 * 32 * 4 + 256 * 256 * 3
     assert sum(g["launches"] for g in groups.values()) == L - 1
+
+
+def test_bench_groups_chain_runs():
+    """A wino_chain_kernel launch (encode_res_1/conv_0 .. encode_4 with the quantiser, and
+    decode_4 .. decode_res_2/conv_1) is ONE group: the Winograd-form FLOPs of all five
+    layers, HBM bytes = the first layer's f32 input + the last layer's output (u8 symbols on
+    the encoder side), the step's rows counting every layer inside in the Winograd form."""
+    import importlib.util
+    import os
+    import numpy as np
+    from tf_image_compression_amd.topology import layer_table, layer_work
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    names = [lay.name for lay in layer_table(0)]
+    L = len(names)
+    kernels = [f"k{i}" for i in range(L)]
+    e0, d0 = names.index("encode_res_1/conv_0"), names.index("decode_4")
+    kernels[e0], kernels[d0] = "wino_chain_kernel<0,1,2>", "wino_chain_kernel<1,0,2>"
+    for i in list(range(e0 + 1, e0 + 5)) + list(range(d0 + 1, d0 + 5)):
+        kernels[i] = ""
+    groups, rows = bench.kernel_groups(None, 0, 256, np.full(L, 0.01), kernels)
+    chains = [g for g in groups.values() if len(g["layers"]) == 5]
+    assert [g["layers"][0] for g in chains] == ["encode_res_1/conv_0", "decode_4"]
+    work = layer_work(0, 256)
+    for g, start in zip(chains, (e0, d0)):
+        assert g["launches"] == 1
+        assert g["flops"] == sum(work[i][1] for i in range(start, start + 5)) * bench.WINO_FRAC
+    hw = 16 * 16 * 64
+    assert chains[0]["bytes"] == hw * 4 + hw      # f32 in, u8 symbols out
+    assert chains[1]["bytes"] == hw + hw * 4      # u8 symbols in, f32 out
+    assert all(rows[i]["flops_per_patch"] == work[i][1] * bench.WINO_FRAC for i in range(e0, e0 + 5))
+    assert sum(g["launches"] for g in groups.values()) == L - 8
