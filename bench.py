@@ -83,7 +83,8 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
     layer whose kernel name is '' ran inside the previous layer's launch (enc01_kernel,
     dec10_kernel: a pair; wino_chain_kernel: a run of stride-1 layers): the launch is one
     group, its work the sum of its layers and its HBM bytes the first layer's input plus the
-    last layer's output (the intermediate activations and residual inputs stay on chip).
+    last layer's output (the intermediate activations and residual inputs stay on chip); its
+    time is the launch's (the layers inside have only an empty event pair of their own).
     A layer inside a Winograd launch counts the Winograd form's FLOPs."""
     from tf_image_compression_amd.topology import layer_work, RMBE_ID, weight_bytes
     work = layer_work(model_id, P)
@@ -128,8 +129,7 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
             nl, nf, _, _ = work[j]
             f += nf
             wb += weight_bytes(nl)
-            t += float(ms[j])
-            names.append(nl.name)
+            names.append(nl.name)  # its own ms is only the event pair recorded after the launch
             key = key + ("fused", nl.name)
         if j > i:  # first layer's input + last layer's output
             o_i, r_i = out_res_bytes(i)
