@@ -122,6 +122,12 @@ int tic_model_layer(int model_id, int i, char* name_buf, int name_len, int* kind
  * tic_codec_device(n) (or the rmbe net); writes the mean ms per launch of layer i to
  * ms_out[i] (size >= tic_num_layers). */
 int tic_profile_layers(tic_handle* h, const void* d_in, int n, int iters, float* ms_out);
+/* In-step launch timing (bench.py's roofline): with option "mark_layer" = i (>= 0) every
+ * lane records a HIP event pair on its own stream around each launch that starts at layer i
+ * (a fused or chained launch starts at its first layer) during ordinary tic_codec_device /
+ * encode / decode calls, up to 1024 pairs per lane.  tic_mark_durations synchronises,
+ * writes up to cap durations (ms) to ms_out, returns how many, and clears the record. */
+int tic_mark_durations(tic_handle* h, float* ms_out, int cap);
 
 /* Measure every compiled tiling of every layer on the live buffers of one encode+decode
  * (or rmbe) pass over d_in[n] and keep the fastest per layer for batch size n (like

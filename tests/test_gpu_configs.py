@@ -240,6 +240,40 @@ def test_graph_replay_after_workspace_growth():
         c.set_option("graph", 0)
 
 
+@pytest.mark.parametrize("mark", ["encode_0", "encode_res_1/conv_0", "decode_1", "encode_3"])
+def test_mark_layer_in_step_timing(mark):
+    """bench.py's in-step launch timing (option mark_layer + tic_mark_durations): one event
+    pair per lane per call around the launch that starts at the marked layer — a fused
+    pair, a chain run or a plain layer — and the results stay bit-identical."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.topology import layer_table
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    P, n, calls = 64, 8, 5
+    names = [lay.name for lay in layer_table(0)]
+    with Codec(0, synthetic_params(0), SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
+        c.set_option("fuse01", 1)
+        c.set_option("fuse_tail", 1)
+        c.set_option("chain", 1)
+        x = structured_patches(n, P, seed=520)
+        eh, ew, ec = c.code_shape
+        d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(n * eh * ew * ec), c.alloc(x.nbytes)
+        d_in.upload(x)
+        c.codec_device(d_in, n, d_idx, d_rgb)
+        c.synchronize()
+        ref = d_idx.download((n, eh, ew, ec), np.uint8), d_rgb.download(x.shape, np.uint8)
+        c.set_option("mark_layer", names.index(mark))
+        for _ in range(calls):
+            c.codec_device(d_in, n, d_idx, d_rgb)
+        ms = c.mark_durations()
+        assert len(ms) == calls * 2 and np.all(ms > 0) and np.all(ms < 50), ms  # two lanes
+        assert len(c.mark_durations()) == 0  # cleared
+        assert np.array_equal(d_idx.download((n, eh, ew, ec), np.uint8), ref[0])
+        assert np.array_equal(d_rgb.download(x.shape, np.uint8), ref[1])
+        c.set_option("mark_layer", -1)
+        c.codec_device(d_in, n, d_idx, d_rgb)
+        assert len(c.mark_durations()) == 0
+
+
 @pytest.mark.parametrize("decouple", [0, 1])
 def test_lane_decoupling_orders_stream_work(decouple):
     """Lanes fork from the handle stream only when it has new work (option "decouple"):

@@ -50,6 +50,7 @@ SIGNATURES = [
     ("tic_model_num_layers", C.c_int, [C.c_int]),
     ("tic_model_layer", C.c_int, [C.c_int, C.c_int, C.c_char_p, C.c_int, i32p, i32p, i32p, i32p, i32p, i32p]),
     ("tic_profile_layers", C.c_int, [vp, vp, C.c_int, C.c_int, f32p]),
+    ("tic_mark_durations", C.c_int, [vp, f32p, C.c_int]),
     ("tic_autotune", C.c_int, [vp, vp, C.c_int, C.c_int]),
     ("tic_layer_variant", C.c_int, [vp, C.c_int, C.c_int, i32p, i32p]),
     ("tic_autotune_step", C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int]),

@@ -185,6 +185,13 @@ class Codec:
         check(lib().tic_profile_layers(self._h, d_in.ptr, n, iters, ptr(ms, C.c_float)), "tic_profile_layers")
         return ms
 
+    def mark_durations(self, cap: int = 8192) -> np.ndarray:
+        """ms of every launch recorded under option "mark_layer" since the last call (all
+        lanes, in-step: tic_mark_durations)."""
+        ms = np.zeros(cap, F32)
+        k = check(lib().tic_mark_durations(self._h, ptr(ms, C.c_float), cap), "tic_mark_durations")
+        return ms[:k]
+
     def autotune(self, d_in: DeviceBuffer, n: int, reps: int = 5) -> None:
         check(lib().tic_autotune(self._h, d_in.ptr, n, reps), "tic_autotune")
 

@@ -356,6 +356,9 @@ struct Lane {
   // timing probes: per slot (0 / 1 the encoder- / decoder-side chain launch, TIC_CHAIN_TIMING;
   // 2 enc01, TIC_ENC01_TIMING) the phase timestamps of the last launch, [grid][stamps]
   unsigned long long* tstamp[3] = {nullptr, nullptr, nullptr};
+  // "mark_layer" timing: event pairs around the marked launch, recorded in call order
+  std::vector<hipEvent_t> mark_ev;
+  int mark_n = 0;
   int tstamp_grid[3] = {0, 0, 0}, tstamp_n[3] = {tic::CH_TS, tic::CH_TS, 8};
 };
 
@@ -398,6 +401,7 @@ struct tic_handle {
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
+  int mark_layer = -1;     // tic_mark_durations: time the launches starting at this layer
   // Lane scheduling: lanes join into `stream` after every call, but wait on it (fork) only
   // when something else was enqueued there since their last fork ("decouple"), so lane k's
   // next batch starts as soon as lane k is free instead of after the slowest lane.
@@ -666,6 +670,8 @@ static bool any_chain(const tic_handle* h) {
 
 // Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
 // outputs per-position flags.  Buffers rotate through h->ws.
+static constexpr int kMarkCap = 1024;  // event pairs per lane
+
 int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, uint8_t* d_idx, float* d_pre,
                uint8_t* d_rgb, float* d_f32, const Prof& prof) {
   hipStream_t const st = ln.stream;
@@ -677,7 +683,21 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
   // whose launch is left out, to price a group of layers inside the whole step
   unsigned long long probe_skip = 0;
   if (const char* s = getenv("TIC_PROBE_SKIP")) probe_skip = strtoull(s, nullptr, 0);
+  int marked = -1;  // event pair open around the launch of layer mark_layer
+  auto mark_close = [&]() -> int {
+    if (marked >= 0) {
+      HIP_TRY(hipEventRecord(ln.mark_ev[2 * marked + 1], st));
+      ++ln.mark_n;
+      marked = -1;
+    }
+    return TIC_OK;
+  };
   for (int li = l0; li < l1; ++li) {
+    if (marked >= 0 && mark_close()) return TIC_EHIP;  // the marked launch was enqueued last
+    if (li == h->mark_layer && !prof.ev && ln.mark_n < (int)ln.mark_ev.size() / 2) {
+      marked = ln.mark_n;
+      HIP_TRY(hipEventRecord(ln.mark_ev[2 * marked], st));
+    }
     LayerRT& lay = h->layers[li];
     const LayerDef& d = lay.def;
     const bool first = li == 0;
@@ -944,7 +964,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
     if (d.residual) block_in = -1;
     cur = dst;
   }
-  return TIC_OK;
+  return mark_close();
 }
 
 int check_ready(tic_handle* h) {
@@ -1177,6 +1197,8 @@ void tic_destroy(tic_handle* h) {
     if (ln.ctl) (void)hipFree(ln.ctl);
     for (auto* t : ln.tstamp)
       if (t) (void)hipFree(t);
+    for (auto e : ln.mark_ev)
+      if (e) (void)hipEventDestroy(e);
   }
   for (int i = 0; i < 4; ++i) {
     if (h->lanes[i].stream) {
@@ -1417,9 +1439,43 @@ int tic_codec_device(tic_handle* h, const uint8_t* d_patches, int n, uint8_t* d_
   return TIC_OK;
 }
 
+int tic_mark_durations(tic_handle* h, float* ms_out, int cap) {
+  if (!h || (!ms_out && cap > 0)) return fail(TIC_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  int k = 0;
+  for (Lane& ln : h->lanes) {
+    HIP_TRY(hipStreamSynchronize(ln.stream));
+    for (int i = 0; i < ln.mark_n; ++i) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, ln.mark_ev[2 * i], ln.mark_ev[2 * i + 1]));
+      if (k < cap) ms_out[k] = ms;
+      ++k;
+    }
+    ln.mark_n = 0;
+  }
+  return std::min(k, cap);
+}
+
 int tic_set_option(tic_handle* h, const char* key, int value) {
   if (!h || !key) return fail(TIC_EINVAL, "null argument");
   const std::string k(key);
+  if (k == "mark_layer") {  // tic_mark_durations: time the launches starting at layer `value`
+    if (value >= (int)h->layers.size()) return fail(TIC_EINVAL, "mark_layer %d out of range", value);
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    for (Lane& ln : h->lanes) {
+      HIP_TRY(hipStreamSynchronize(ln.stream));
+      ln.mark_n = 0;
+      if (value >= 0 && ln.mark_ev.empty()) {
+        ln.mark_ev.resize(2 * kMarkCap, nullptr);
+        for (auto& e : ln.mark_ev) HIP_TRY(hipEventCreate(&e));
+      }
+    }
+    h->mark_layer = value < 0 ? -1 : value;
+    return TIC_OK;
+  }
   if (k == "streams") {
     if (value < 1 || value > 4) return fail(TIC_EINVAL, "streams must be 1..4");
     HIP_TRY(hipStreamSynchronize(h->stream));
