@@ -693,7 +693,9 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
     return TIC_OK;
   };
   for (int li = l0; li < l1; ++li) {
-    if (marked >= 0 && mark_close()) return TIC_EHIP;  // the marked launch was enqueued last
+    if (marked >= 0) {  // the marked launch was the last one enqueued
+      if (int rc = mark_close()) return rc;
+    }
     if (li == h->mark_layer && !prof.ev && ln.mark_n < (int)ln.mark_ev.size() / 2) {
       marked = ln.mark_n;
       HIP_TRY(hipEventRecord(ln.mark_ev[2 * marked], st));
