@@ -15,8 +15,9 @@
 // transform points (xi, 0..3)); the region's 10x10 input tile (1-pixel halo) stays in LDS
 // from layer to layer.  Between layers a region needs its neighbours' border pixels: each
 // workgroup publishes its 32 border pixels (rows 0 and 7, columns 0 and 7; 8 KB) with
-// write-through (sc1) 8-byte stores, drains them, and raises a per-(layer, region) flag;
-// the neighbours poll the flags with sc1 loads and read the halo with sc1 loads
+// write-through (sc1) 16-byte buffer stores, drains them, and raises a per-(layer, region)
+// flag; the neighbours poll the flags with sc1 loads and read the halo with 16-byte sc1
+// buffer loads
 // (MI355X_MICROARCH.md, valid hand-off form, row 1).  No redundant halo recomputation,
 // ~1 hand-off per layer instead of a kernel boundary + full activation round trip.
 //
@@ -78,21 +79,22 @@ constexpr unsigned kSpinLimit = 1u << 19;  // ~0.5 s of polling before the error
 // LDS float offset of staged pixel (row, col) of a 10x10 tile (columns split by parity)
 __device__ __forceinline__ int tpix(int row, int col) { return (row * RP + (col & 1) * HP + (col >> 1)) * PS; }
 
-__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
-  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-  const unsigned long long lo = (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32);
-  const unsigned long long hi = (unsigned long long)__float_as_uint(v.z) | ((unsigned long long)__float_as_uint(v.w) << 32);
-  __hip_atomic_store(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// 16-byte write-through (sc1) store / sc1 load through a buffer resource (aux 16 = sc1):
+// one buffer_store/load_dwordx4 instead of two 8-byte atomics (MI355X_MICROARCH.md: 8-B
+// accesses run at 0.54-0.70x the 16-B rate; hand-off table row 1 allows 16-B sc1 both sides)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xrsrc(const float* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1_16(__amdgpu_buffer_rsrc_t r, int byte_off, f32x4 v) {
+  const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, byte_off, 0, 16);
+}
+__device__ __forceinline__ f32x4 ld_sc1_16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+  return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
 }
 
-__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
-  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
-  const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return f32x4{__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)), __uint_as_float((unsigned)hi),
-               __uint_as_float((unsigned)(hi >> 32))};
-}
 }  // namespace chain
 
 // IN: IN_F32 / IN_IDX for the first layer; OUT: OUT_F32 / OUT_QUANT for the last one.
@@ -359,12 +361,13 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     if (R > 1 && a.probe != 1) {
       const size_t g = (size_t)nimg * R + reg;
       float* const xb = a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C);
+      const __amdgpu_buffer_rsrc_t rpub = xrsrc(xb, 4 * 8 * C * 4);  // this region's 8 KB border
 #pragma unroll
       for (int k = 0; k < 512 / NTH; ++k) {  // 4 sides x 8 pixels x 16 quads = 512 chunks
         const int e = k * NTH + tid;
         const int side = e >> 7, px = (e >> 4) & 7, q = e & 15;
         const int ly = side == 0 ? 0 : (side == 1 ? 7 : px), lx = side == 2 ? 0 : (side == 3 ? 7 : px);
-        st_sc1(xb + (side * 8 + px) * C + 4 * q, *reinterpret_cast<const f32x4*>(&dst[tpix(ly + 1, lx + 1) + 4 * q]));
+        st_sc1_16(rpub, ((side * 8 + px) * C + 4 * q) * 4, *reinterpret_cast<const f32x4*>(&dst[tpix(ly + 1, lx + 1) + 4 * q]));
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -388,6 +391,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       __syncthreads();
       stamp(ts + 4);
       // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16 quads
+      const __amdgpu_buffer_rsrc_t rlay = xrsrc(a.xbuf + (size_t)l * nR * (4 * 8 * C), (unsigned)nR * (4 * 8 * C * 4));
       for (int e = tid; e < 36 * 16; e += NTH) {
         const int hp = e >> 4, q = e & 15;
         int hy, hx;
@@ -405,8 +409,8 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
           else if (hy > 7) side = 0, idx = nx;
           else if (hx < 0) side = 3, idx = ny;
           else side = 2, idx = ny;
-          const size_t gn = (size_t)nimg * R + nry * a.rw + nrx;
-          v = ld_sc1(a.xbuf + ((size_t)l * nR + gn) * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q);
+          const int gn = nimg * R + nry * a.rw + nrx;
+          v = ld_sc1_16(rlay, (gn * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q) * 4);
         }
         *reinterpret_cast<f32x4*>(&dst[tpix(hy + 1, hx + 1) + 4 * q]) = v;
       }
