@@ -53,8 +53,12 @@ def parse():
                          "matches these kernel sources and its configuration matches this run")
     ap.add_argument("--tune-cache", default="auto",
                     help="tuning state (tic_tuning_export) to replay instead of tuning: 'auto' = the "
-                         "committed tools/tune/<config>.json when its source stamp matches (else tune), "
+                         "shipped tf_image_compression_amd/tune/<config>.json when its source stamp "
+                         "matches (else tune), "
                          "'none' = always tune, PATH = load if present and matching, else tune and save")
+    ap.add_argument("--tune-save", default=None,
+                    help="directory: save every state tuned in this run there under its canonical "
+                         "name (model{M}_p{P}_b{B}_s{S}.json), for tf_image_compression_amd/tune/")
     ap.add_argument("--trace-only", action="store_true",
                     help="stop after the timed steps (for rocprofv3 timelines of the steady state)")
     ap.add_argument("--pmc-plan", default=None,
@@ -62,15 +66,21 @@ def parse():
                          "steps on ONE lane at the per-lane batch (deterministic dispatch order), write "
                          "the launch plan of one step to this path, print nothing else")
     ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
-    ap.add_argument("--workload", choices=["patches", "image4k"], default="patches",
+    ap.add_argument("--workload", choices=["patches", "image4k", "sharded"], default="patches",
                     help="patches: BASELINE configs[1]/[2] (default); image4k: configs[4], whole "
-                         "3840x2160 images tiled 256x256 -> model_3 -> stitch -> rmbe post-filter -> u8")
-    ap.add_argument("--images", type=int, default=1, help="image4k: images per rank per step")
+                         "3840x2160 images tiled 256x256 -> model_3 -> stitch -> rmbe post-filter -> u8; "
+                         "sharded: configs[3], a synthetic image set split over the ranks, resident in "
+                         "HBM, one step = one pass over every rank's shard + exact SSE + stats all-gather")
+    ap.add_argument("--images", type=int, default=None,
+                    help="image4k: images per rank per step (default 1); sharded: images in the whole "
+                         "set (default 10000)")
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--width", type=int, default=3840)
     args = ap.parse_args()
     if args.workload == "image4k" and "--model" not in sys.argv:
         args.model = 3
+    if args.images is None:
+        args.images = 10000 if args.workload == "sharded" else 1
     if args.traffic is None:
         # committed PMC summaries exist per model (tools/pmc); none for models 1/2 -> None
         name = {0: "traffic_model0.json", 3: "traffic_model3.json"}.get(args.model)
@@ -317,6 +327,8 @@ def main():
     args = parse()
     if args.workload == "image4k":
         return main_image(args)
+    if args.workload == "sharded":
+        return main_sharded(args)
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
     from tf_image_compression_amd.topology import bottleneck_shape, layer_table
@@ -329,7 +341,8 @@ def main():
             print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     P, B, M = args.patch, args.batch, args.model
     params = synthetic_params(M, seed=0)
-    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local)
+    # tuning="none": bench.py replays (or re-measures) the tuning state itself, below
+    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local, tuning="none")
     codec.set_option("streams", args.streams)
     codec.set_option("graph", 1 if args.graph else 0)
     comm = dist.make_comm(codec)
@@ -495,20 +508,24 @@ def main():
 
 
 def tune_cache_path(args, M, P, B):
+    """(state to replay if present and matching, where to save a state tuned in this run)."""
+    from tf_image_compression_amd import tuning
+    name = os.path.basename(tuning.tune_path(M, P, B, args.streams))
+    save = os.path.join(args.tune_save, name) if args.tune_save else None
     if args.tune_cache == "none":
-        return None, False
+        return None, save
     if args.tune_cache == "auto":
-        return os.path.join(ROOT, "tools", "tune", f"model{M}_p{P}_b{B}_s{args.streams}.json"), False
-    return args.tune_cache, True
+        return tuning.tune_path(M, P, B, args.streams), save
+    return args.tune_cache, save or args.tune_cache
 
 
 def tune(args, codec, d_in, B, lane_b, M, P):
     """Per-layer autotune + in-situ step tuning (outside the timed region), or the replay of
-    a saved tuning state of the same kernel sources and configuration."""
-    from tf_image_compression_amd._lib import source_digest
+    the shipped tuning state (tf_image_compression_amd/tune/, the same file Codec applies by
+    default) when it was measured on these kernel sources and this configuration."""
+    from tf_image_compression_amd import tuning
     path, save = tune_cache_path(args, M, P, B)
-    stamp = {"source_sha256": source_digest(), "model": M, "patch": P, "batch": B, "streams": args.streams,
-             "tune_step": args.tune_step}
+    stamp = tuning.stamp(M, P, B, args.streams, args.tune_step)
     if path and os.path.exists(path):
         doc = json.load(open(path))
         if doc.get("_meta") == stamp:
@@ -517,9 +534,9 @@ def tune(args, codec, d_in, B, lane_b, M, P):
     codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice
     if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
         codec.autotune_step(d_in, B, rounds=args.tune_step, reps=5)
-    if path and save:
-        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-        json.dump({"_meta": stamp, "tuning": codec.tuning_export()}, open(path, "w"), indent=1)
+    if save:
+        os.makedirs(os.path.dirname(os.path.abspath(save)), exist_ok=True)
+        json.dump({"_meta": stamp, "tuning": codec.tuning_export()}, open(save, "w"), indent=1)
     return "tuned in this run"
 
 
@@ -548,6 +565,100 @@ def pmc_steady(args, codec, d_in, d_idx, d_rgb, lane_b, M, P):
             "libtic_sha256": lib_digest(), "streams_in_bench": args.streams}
     os.makedirs(os.path.dirname(os.path.abspath(args.pmc_plan)), exist_ok=True)
     json.dump({"_meta": meta, "plan": plan}, open(args.pmc_plan, "w"), indent=1)
+    codec.close()
+
+
+def main_sharded(args):
+    """BASELINE configs[3]: a synthetic set of args.images 256x256 images split statically
+    over the ranks (dist.shard_range), each rank's shard resident in HBM (uploaded before
+    the timed region), one step = one pass of tic_codec_device over the shard in batches of
+    args.batch (the shipped tuning) + the exact SSE kernel; after the timed steps ONE RCCL
+    all-gather of the per-rank stats gives the dataset PSNR (processing_utils/evaluate.py:
+    18-32).  value = images x P^2 of all ranks x steps / max-over-ranks time."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    from tf_image_compression_amd.topology import bottleneck_shape
+    from tf_image_compression_amd import dist, sharded
+
+    rank, world, local = dist.env_rank()
+    P, B, M, NI = args.patch, args.batch, args.model, args.images
+    params = synthetic_params(M, seed=0)
+    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local, tuning="none")
+    codec.set_option("streams", args.streams)
+    comm = dist.make_comm(codec)
+    eh, ew, ec = bottleneck_shape(M, P)
+    lo, hi = dist.shard_range(NI, rank, world)
+    t_gen = time.perf_counter()
+    shard = sharded.DeviceShard(codec, sharded.shard_images(NI, rank, world, P, "uniform"), B)
+    t_gen = time.perf_counter() - t_gen
+    lane_b = -(-B // max(1, min(args.streams, B)))
+    tuning = "none"
+    if not args.no_autotune and shard.n >= B:
+        tuning = tune(args, codec, shard.d_img, B, lane_b, M, P)
+    for _ in range(args.warmup):
+        shard.enqueue()
+    codec.synchronize()
+    comm.barrier()
+    codec.synchronize()
+    t0 = time.perf_counter()
+    wall0 = time.time()
+    for _ in range(args.steps):
+        shard.enqueue()
+    codec.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    wall1 = time.time()
+    t_max = comm.allreduce_max(elapsed)
+    st = shard.stats(args.steps, wall0, wall1)
+    summary = dist.combine(comm.allgather_stats(st))
+    # the one-lane roofline of the dominant launch group at the shard's batch (as configs[1])
+    ms = codec.profile_layers(shard.d_img, lane_b, args.profile_iters) if shard.n >= lane_b else None
+    roof = None
+    if ms is not None:
+        kernels = codec.layer_kernels(lane_b)
+        groups, _ = kernel_groups(codec, M, P, ms, kernels)
+        dom_key = max(groups, key=lambda k: groups[k]["ms"])
+        roof, dom_ms, dom_flops, _ = roofline_of(groups[dom_key], lane_b)
+        from tf_image_compression_amd.topology import layer_table
+        names = {lay.name: i for i, lay in enumerate(layer_table(M))}
+        dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
+        winograd_note(roof, dom_kernels, dom_flops, dom_ms)
+        roof.update(pmc_traffic(args.traffic, launch_units(groups[dom_key]["layers"], kernels, names),
+                                {"model": M, "patch": P, "lane_batch": lane_b}))
+        roof["kernel"] = "+".join(groups[dom_key]["layers"])
+        roof["kernel_instance"] = dom_kernels
+        roof["ms_per_launch"] = round(dom_ms, 5)
+        roof["timing"] = "one-lane per-layer HIP events (profile_layers)"
+    step_ms = t_max * 1e3 / args.steps
+    value = NI * P * P * args.steps / t_max / 1e6
+    out = {
+        "metric": "encode+decode MPix/s at 256x256 RGB",
+        "value": round(value, 2),
+        "unit": "MPix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_ms, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic uniform u8 images (seeded by global image index), seeded He-normal weights",
+        "config": {"workload": f"model_{M}, {NI}-image synthetic set of {P}x{P} RGB sharded over {world} GPU(s), "
+                               f"batches of {B}, RCCL stats all-gather (BASELINE configs[3])",
+                   "model": f"model_{M}", "images": NI, "images_per_rank": hi - lo, "patch": P, "batch": B,
+                   "code_shape": [eh, ew, ec], "parallelism": f"image-parallel x{world}"},
+        "roofline": roof,
+        "lanes": {"streams": args.streams, "patches_per_launch": lane_b},
+        "tuning": tuning,
+        "shard_upload_s": round(t_gen, 2),
+        "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
+                            "raw_bpp": round(summary["bpp"], 4), "per_step_images": summary["images"] // args.steps},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    shard.free()
+    comm.close()
     codec.close()
 
 
@@ -607,8 +718,8 @@ def main_image(args):
     P, M, H, W, NI = args.patch, args.model, args.height, args.width, args.images
     params = synthetic_params(M, seed=0)
     rparams = synthetic_params(RMBE_ID, seed=0)
-    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local)
-    post = Codec(RMBE_ID, rparams, SYNTH_MEAN, SYNTH_STD, patch_size=128, device=local)
+    codec = Codec(M, params, SYNTH_MEAN, SYNTH_STD, patch_size=P, quan_scale=2, device=local, tuning="none")
+    post = Codec(RMBE_ID, rparams, SYNTH_MEAN, SYNTH_STD, patch_size=128, device=local, tuning="none")
     for c in (codec, post):
         c.set_option("streams", args.streams)
     comm = dist.make_comm(codec)
@@ -625,14 +736,18 @@ def main_image(args):
 
     lane_b = -(-npat // max(1, min(args.streams, npat)))
     n_win = (H // 128) * ((W - 64) // 128) + ((H - 64) // 128) * (W // 128)
-    win_lane = -(-min(n_win, 256) // max(1, min(args.streams, min(n_win, 256))))
+    win_b = min(n_win, 256)  # rmbe windows per launch sequence (the handle's chunk)
+    win_lane = -(-win_b // max(1, min(args.streams, win_b)))
     d_pat = codec.alloc(npat * P * P * 3)
     codec.image_to_patches_device(d_img[0], H, W, P, d_pat)
-    d_win = post.alloc(win_lane * 128 * 128 * 3 * 4)
-    d_win.upload(r.random((win_lane, 128, 128, 3), dtype=np.float32) * 255)
+    d_win = post.alloc(win_b * 128 * 128 * 3 * 4)
+    d_win.upload(r.random((win_b, 128, 128, 3), dtype=np.float32) * 255)
+    tuning = {"codec": "none", "rmbe": "none"}
     if not args.no_autotune:
-        codec.autotune(d_pat, lane_b, reps=5)
-        post.autotune(d_win, win_lane, reps=5)
+        # both networks tuned like configs[1]: per-layer autotune + the whole-step tuner
+        # (fusions, chain, variants), or the replay of the shipped state for this shape
+        tuning["codec"] = tune(args, codec, d_pat, npat, lane_b, M, P)
+        tuning["rmbe"] = tune(args, post, d_win, win_b, win_lane, RMBE_ID, 128)
 
     def step():
         for i in range(NI):
@@ -713,6 +828,7 @@ def main_image(args):
         "roofline": roof,
         "roofline_step_frac": round(t_min * NI * 1e3 / step_ms, 4),
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "windows_per_launch": win_lane},
+        "tuning": tuning,
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
                             "raw_bpp": round(summary["bpp"], 4)},
     }

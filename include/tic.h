@@ -105,7 +105,14 @@ int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out);
  * patches per launch sequence, default 256, env TIC_MAX_CHUNK), "graph" (1: replay
  * tic_codec_device as a captured HIP graph per (buffers, n) — default 0: measured slower
  * than eager dual-lane launches on MI355X), "persist_grid" (> 0: cap on the grid of the
- * persistent conv variants, so that tests run several tiles per workgroup; default 0). */
+ * persistent conv variants, so that tests run several tiles per workgroup; default 0).
+ * Structural, bit-identical fusions (1 on, 0 off, -1 the model's default): "fuse01"
+ * (encode_0 + encode_1 in one launch; default on), "fuse_tail" (decode_1 + decode_0; on),
+ * "chain" (each run of stride-1 64->64 layers in one launch; on for models 0-2, off for
+ * model_3 / rmbe; declined automatically where the geometry cannot run it), "chain_wh"
+ * (1 or 2), "s1_form" (0 direct, 1 Winograd, -1 default), "decouple" (lanes fork from the
+ * handle stream only when a call's device byte ranges or earlier non-lane work require it;
+ * default 1), "mark_layer" (see tic_mark_durations). */
 int tic_set_option(tic_handle* h, const char* key, int value);
 
 /* --- introspection / measurement --- */

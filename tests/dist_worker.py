@@ -17,14 +17,22 @@ from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH
 
 def main():
     out, n_images, P = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    driver = sys.argv[4] if len(sys.argv) > 4 else "host"
     comm = dist.GlooComm()
     params = synthetic_params(1)
 
-    def codec_fn(x):
-        _, idx = o.encoder(params, SYNTH_MEAN, SYNTH_STD, x, P, 2, 1)
-        return o.decoder(params, SYNTH_MEAN, SYNTH_STD, idx, 2, 1)[1]
+    if driver == "device":  # the GPU driver's orchestration (sharded.run_device_shard)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from host_codec import HostCodec
+        codec = HostCodec(1, params, SYNTH_MEAN, SYNTH_STD, P)
+        _, st = sharded.run_device_shard(codec, comm, comm.rank, comm.world, n_images, batch=3)
+        assert codec.calls == -(-st.images // 3)
+    else:
+        def codec_fn(x):
+            _, idx = o.encoder(params, SYNTH_MEAN, SYNTH_STD, x, P, 2, 1)
+            return o.decoder(params, SYNTH_MEAN, SYNTH_STD, idx, 2, 1)[1]
 
-    st = sharded.run_shard(codec_fn, comm.rank, comm.world, n_images, P, 3, (P // 16) ** 2 * 64)
+        st = sharded.run_shard(codec_fn, comm.rank, comm.world, n_images, P, 3, (P // 16) ** 2 * 64)
     stats = comm.allgather_stats(st)
     tmax = comm.allreduce_max(float(comm.rank + 1))
     # TCP bootstrap of the 128-byte RCCL unique id (same code path as RcclComm)

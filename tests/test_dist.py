@@ -47,14 +47,19 @@ def _free_port():
     return p
 
 
-def test_gloo_world2_sharded_stats(tmp_path):
+@pytest.mark.parametrize("driver", ["host", "device"])
+def test_gloo_world2_sharded_stats(tmp_path, driver):
+    """Both shard drivers over gloo at world size 2: "host" (run_shard) and "device"
+    (run_device_shard, the GPU path's orchestration: resident shard, batches at buffer
+    offsets, one SSE reduction, one all-gather) with tests/host_codec.py standing in for
+    the GPU codec."""
     n, P = 7, 32
     port = _free_port()
     out = str(tmp_path / "res")
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "dist_worker.py"),
-           out, str(n), str(P)]
+           out, str(n), str(P), driver]
     subprocess.run(cmd, check=True, env=env, timeout=240, cwd=ROOT)
     res = [json.load(open(f"{out}.{r}")) for r in range(2)]
     assert res[0]["summary"] == res[1]["summary"]

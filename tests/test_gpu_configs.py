@@ -134,9 +134,11 @@ def test_image_4k_properties(m3_256, rmbe_codec):
 
 
 def test_sharded_world1_gpu():
-    """configs[3] orchestration at world size 1 on the GPU: run_shard over 70 synthetic
-    images (two batches of 64), dataset PSNR within 0.02 dB of the oracle's on the same
-    images, counts exact."""
+    """configs[3] orchestration at world size 1 on the GPU, device-resident
+    (sharded.run_device_shard: the shard uploaded once, tic_codec_device per batch of 64 at
+    buffer offsets, the exact SSE kernel, one all-gather): 70 synthetic images (a full and a
+    partial batch), dataset PSNR within 0.02 dB of the oracle's on the same images, counts
+    exact, and the device SSE equal to the host path's."""
     from tf_image_compression_amd import dist, sharded
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.topology import bottleneck_shape
@@ -146,10 +148,11 @@ def test_sharded_world1_gpu():
     eh, ew, ec = bottleneck_shape(0, P)
     with Codec(0, params, SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
         comm = dist.make_comm(c)
-        st = sharded.run_shard(lambda x: c.decode(c.encode(x)), 0, 1, n, P, 64, eh * ew * ec)
-        summary = dist.combine(comm.allgather_stats(st))
+        summary, st = sharded.run_device_shard(c, comm, 0, 1, n, batch=64, passes=2)
+        host = sharded.run_shard(lambda x: c.decode(c.encode(x)), 0, 1, n, P, 64, eh * ew * ec)
         comm.close()
-    assert summary["images"] == n and st.dims == n * P * P * 3 and st.bits == n * eh * ew * ec
+    assert summary["images"] == 2 * n and st.dims == 2 * n * P * P * 3 and st.bits == 2 * n * eh * ew * ec
+    assert st.sse == 2 * host.sse
     x = sharded.image_batch(0, n, P)
     _, idx = o.encoder(params, SYNTH_MEAN, SYNTH_STD, x, P, 2, 0, acc=np.float32)
     _, rec = o.decoder(params, SYNTH_MEAN, SYNTH_STD, idx, 2, 0, acc=np.float32)

@@ -277,7 +277,7 @@ def test_fused_first_layers_bit_identical(lib_codec, monkeypatch, model_id, P):
             idx1, pre1 = codec.encode(x, return_preact=True)
             assert np.array_equal(pre0, pre1) and np.array_equal(idx0, idx1), v
     finally:
-        codec.set_option("fuse01", 0)
+        codec.set_option("fuse01", -1)
 
 
 def test_fused_rmbe_first_layers_bit_identical(monkeypatch):
@@ -370,7 +370,7 @@ def test_fused_tail_bit_identical(lib_codec, monkeypatch, model_id, P):
             monkeypatch.setenv("TIC_DEC10_VARIANT", str(v))
             outs.append(codec.decode(idx, return_float=True))
     finally:
-        codec.set_option("fuse_tail", 0)
+        codec.set_option("fuse_tail", -1)
     for u1, f1 in outs:
         assert np.array_equal(u0, u1) and np.array_equal(f0, f1)
 

@@ -41,17 +41,38 @@ class DeviceBuffer:
         check(lib().tic_memcpy_d2h(self.codec._h, out.ctypes.data, self.ptr, out.nbytes), "tic_memcpy_d2h")
         return out
 
+    def view(self, offset: int) -> "DeviceView":
+        """The same allocation from byte ``offset`` on (a pointer into it, as a C caller
+        would pass one; not owned)."""
+        if not 0 <= offset <= self.nbytes:
+            raise ValueError(f"offset {offset} outside the {self.nbytes}-byte buffer")
+        return DeviceView(self, int(offset))
+
     def free(self) -> None:
         if self.ptr is not None and self.codec._h is not None:
             check(lib().tic_device_free(self.codec._h, self.ptr), "tic_device_free")
         self.ptr = None
 
 
+class DeviceView:
+    """A byte offset into a DeviceBuffer, accepted wherever a DeviceBuffer is (``.ptr``)."""
+
+    def __init__(self, buf: DeviceBuffer, offset: int):
+        self.codec = buf.codec
+        self.base = buf
+        self.offset = offset
+        self.nbytes = buf.nbytes - offset
+        self.ptr = C.c_void_p(buf.ptr.value + offset)
+
+
 class Codec:
     """A model_N codec on one GPU.  ``params``: TF-named float32 arrays (weights.py)."""
 
     def __init__(self, model_id: int, params: dict, mean, std, patch_size: int | None = None,
-                 quan_scale: int = 2, device: int = 0):
+                 quan_scale: int = 2, device: int = 0, tuning: str = "auto"):
+        """``tuning``: "auto" applies the shipped tuning database (tuning.py: the fusions,
+        tilings and variants bench.py measured best for this model / patch / lanes);
+        "none" keeps the runtime's built-in per-model defaults."""
         self.model_id = int(model_id)
         if patch_size is None:
             patch_size = 128 if model_id in (2, 3, CH128_ID, RMBE_ID) else 256
@@ -76,6 +97,12 @@ class Codec:
                 check(lib().tic_set_param(h, name.encode(), ptr(a, C.c_float), shape, a.ndim),
                       f"tic_set_param({name})")
             check(lib().tic_finalize(h), "tic_finalize")
+            self.tuning_source = "runtime defaults"
+            if tuning == "auto":
+                from . import tuning as _tuning
+                self.tuning_source = _tuning.apply(self)
+            elif tuning != "none":
+                raise ValueError(f"tuning must be 'auto' or 'none', got {tuning!r}")
         except Exception:
             self.close()
             raise
@@ -294,4 +321,4 @@ def version() -> str:
     return lib().tic_version().decode()
 
 
-__all__ = ["Codec", "DeviceBuffer", "version", "_lib"]
+__all__ = ["Codec", "DeviceBuffer", "DeviceView", "version", "_lib"]

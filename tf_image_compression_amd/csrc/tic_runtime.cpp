@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -395,7 +396,7 @@ struct tic_handle {
   int tune_reps = 0;  // > 0 while tic_autotune runs
   int num_cus = 256;
   bool use_graph = false;
-  bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); measured slower, opt-in
+  bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); default: struct_defaults
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
@@ -409,6 +410,15 @@ struct tic_handle {
   bool stream_dirty = true;     // non-lane work enqueued on `stream` since the last fork
   bool external_stream = false; // the caller holds the raw stream (tic_get_stream): always fork
   bool force_fork = false;      // tuning / graph capture: every call forks
+  // Device byte ranges the lanes read / wrote since the last fork, by lane.  A call whose
+  // lane i would touch a range another lane wrote (or write one another lane touched) since
+  // then is not ordered after that work by lane i's own stream, so it forks.
+  struct Span {
+    uintptr_t lo, hi;
+    int lane;
+    bool write;
+  };
+  std::vector<Span> spans;
   struct GraphKey {
     const void *in, *idx, *rgb;
     int n, nlanes;
@@ -577,8 +587,19 @@ int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(i
 
 const int kRgbInDefault = 2;   // TH 16
 
-// decoder tail fusion default (option "fuse_tail", env TIC_FUSE_TAIL)
-const bool kFuseTailDefault = false;
+// Structural defaults of a handle (options "fuse01", "fuse_tail", "chain"; value -1 restores
+// them; env TIC_FUSE01 / TIC_FUSE_TAIL / TIC_CHAIN override): the fused pairs everywhere
+// they apply (bit-identical, measured faster for model_0 and model_3 by tic_autotune_step:
+// profiles/tune logs in DESIGN.md §3), the stride-1 chain where the runs are small 16x16
+// stages (model_0/1/2: measured faster) but not for model_3's 64x64 / 32x32 stages or the
+// rmbe net (the step tuner keeps it off there).
+struct StructDefaults {
+  bool fuse01, fuse_tail, chain;
+};
+StructDefaults struct_defaults(int model_id) {
+  const bool small_stages = model_id == 0 || model_id == 1 || model_id == 2;
+  return {true, true, small_stages};
+}
 
 // Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino, else built-in.
 const int kS1FormDefault = 1;
@@ -650,6 +671,16 @@ static int chain_end(const tic_handle* h, int li) {
     return d.kind == K_S1 && d.cin == 64 && d.cout == 64 && i > 0 && i < L - 1;
   };
   if (!s1_64(li)) return li;
+  // Geometry the kernel can run: a region waits for its neighbours, so about rw + 2 regions
+  // of a patch must be resident at once in every lane running a chain (resident slots: one
+  // 512-thread or two 256-thread workgroups per CU; margin 2x), and the hand-off buffer's
+  // byte offsets (n * R * 8 KB, n <= chunk) must fit the 32-bit buffer-resource range.
+  {
+    const int rw = (h->layers[li].h_in + 7) / 8;
+    const long slots = (long)h->num_cus * (h->chain_wh == 1 ? 2 : 1);
+    if ((long)h->nlanes * (2L * rw + 2) > slots) return li;
+    if ((size_t)h->chunk * rw * rw * 8192 > (size_t)INT_MAX) return li;
+  }
   const bool first_dec = !h->rmbe() && li == h->n_enc;
   if (!first_dec && s1_64(li - 1) && (h->rmbe() || li - 1 != h->n_enc - 1)) return li;  // not a run start
   int j = li + 1;
@@ -981,10 +1012,18 @@ size_t code_elems(const tic_handle* h) {
   return (size_t)l.h_out * l.h_out * l.def.cout;
 }
 
+// A per-patch device buffer a chunked call touches: patch p occupies [base + p*pp, +pp).
+struct PatchBuf {
+  const void* base;
+  size_t pp;  // bytes per patch
+  bool write;
+};
+
 // chunked drivers (device pointers).  Each chunk runs on lane 0, or is split in halves
 // over nlanes lanes in near-equal parts (fork/join with events on the handle's stream).
+// `s` is the chunk's first patch; `bufs` the per-patch buffers the call reads / writes.
 template <typename F>
-int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
+int run_chunk(tic_handle* h, int s, int m, bool allow_split, const PatchBuf* bufs, int nbufs, F&& body) {
   const int k = allow_split ? std::min(h->nlanes, m) : 1;
   int part[4], off[4];
   for (int i = 0, o = 0; i < k; ++i) {
@@ -996,14 +1035,45 @@ int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
     int rc = ensure_ws(h, h->lanes[i], part[i]);
     if (rc) return rc;
   }
-  const bool fork = !h->decouple || h->stream_dirty || h->external_stream || h->force_fork || h->tune_reps > 0;
+  // this call's spans, by lane
+  std::vector<tic_handle::Span> mine;
+  for (int i = 0; i < k; ++i)
+    for (int b = 0; b < nbufs; ++b) {
+      if (!bufs[b].base) continue;
+      const uintptr_t lo = (uintptr_t)bufs[b].base + (uintptr_t)(s + off[i]) * bufs[b].pp;
+      mine.push_back({lo, lo + (uintptr_t)part[i] * bufs[b].pp, i, bufs[b].write});
+    }
+  bool fork = !h->decouple || h->stream_dirty || h->external_stream || h->force_fork || h->tune_reps > 0;
+  for (size_t a = 0; a < mine.size() && !fork; ++a)
+    for (const tic_handle::Span& e : h->spans)
+      if (e.lane != mine[a].lane && (e.write || mine[a].write) && e.lo < mine[a].hi && mine[a].lo < e.hi) {
+        fork = true;  // lane work of another lane on these bytes is not ordered before ours
+        break;
+      }
   if (fork) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     for (int i = 0; i < k; ++i) HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
-    // lanes that sit this call out are behind the fork too the next time they run
-    for (int i = k; i < 4; ++i) HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
+    // lanes that sit this call out are behind the fork too the next time they run; they are
+    // joined back at once, so a graph capture never holds an unjoined fork
+    for (int i = k; i < 4; ++i) {
+      HIP_TRY(hipStreamWaitEvent(h->lanes[i].stream, h->ev_fork, 0));
+      HIP_TRY(hipEventRecord(h->ev_join[i], h->lanes[i].stream));
+      HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join[i], 0));
+    }
     h->stream_dirty = false;
+    h->spans.clear();  // every lane is now behind all earlier work
   }
+  for (const tic_handle::Span& sp : mine) {
+    bool merged = false;
+    for (tic_handle::Span& e : h->spans)
+      if (e.lane == sp.lane && e.lo == sp.lo && e.hi == sp.hi) {
+        e.write = e.write || sp.write;
+        merged = true;
+        break;
+      }
+    if (!merged) h->spans.push_back(sp);
+  }
+  if (h->spans.size() > 1024) h->stream_dirty = true;  // bounded: the next call forks and clears
   int rc = TIC_OK;
   for (int i = 0; i < k && !rc; ++i) rc = body(h->lanes[i], off[i], part[i]);
   for (int i = 0; i < k; ++i) {
@@ -1016,9 +1086,10 @@ int run_chunk(tic_handle* h, int m, bool allow_split, F&& body) {
 int encode_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, float* pre, const Prof& prof) {
   const size_t in_pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
   const bool split = !prof.ev && h->tune_reps == 0;
+  const PatchBuf bufs[3] = {{in, in_pp, false}, {idx, ce, true}, {pre, ce * 4, true}};
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = run_chunk(h, m, split, [&](Lane& ln, int o, int k) {
+    int rc = run_chunk(h, s, m, split, bufs, 3, [&](Lane& ln, int o, int k) {
       const int b = s + o;
       return run_layers(h, ln, 0, h->n_enc, in + b * in_pp, k, idx + b * ce, pre ? pre + b * ce : nullptr,
                         nullptr, nullptr, prof);
@@ -1031,9 +1102,10 @@ int encode_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, float* pre
 int decode_dev(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb, float* f32, const Prof& prof) {
   const size_t out_pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
   const bool split = !prof.ev && h->tune_reps == 0;
+  const PatchBuf bufs[3] = {{idx, ce, false}, {rgb, out_pp, true}, {f32, out_pp * 4, true}};
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = run_chunk(h, m, split, [&](Lane& ln, int o, int k) {
+    int rc = run_chunk(h, s, m, split, bufs, 3, [&](Lane& ln, int o, int k) {
       const int b = s + o;
       return run_layers(h, ln, h->n_enc, (int)h->layers.size(), idx + b * ce, k, nullptr, nullptr,
                         rgb ? rgb + b * out_pp : nullptr, f32 ? f32 + b * out_pp : nullptr, prof);
@@ -1046,9 +1118,10 @@ int decode_dev(tic_handle* h, const uint8_t* idx, int n, uint8_t* rgb, float* f3
 // encode -> decode of one chunk back to back on each lane (no join in between)
 int codec_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, uint8_t* rgb) {
   const size_t pp = (size_t)h->P * h->P * 3, ce = code_elems(h);
+  const PatchBuf bufs[3] = {{in, pp, false}, {idx, ce, true}, {rgb, pp, true}};
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = run_chunk(h, m, h->tune_reps == 0, [&](Lane& ln, int o, int k) {
+    int rc = run_chunk(h, s, m, h->tune_reps == 0, bufs, 3, [&](Lane& ln, int o, int k) {
       const int b = s + o;
       int r = run_layers(h, ln, 0, h->n_enc, in + b * pp, k, idx + b * ce, nullptr, nullptr, nullptr, Prof{nullptr});
       if (r) return r;
@@ -1063,9 +1136,10 @@ int codec_dev(tic_handle* h, const uint8_t* in, int n, uint8_t* idx, uint8_t* rg
 int rmbe_dev(tic_handle* h, const float* in, int n, float* out, const Prof& prof) {
   const size_t pp = (size_t)h->P * h->P * 3;
   const bool split = !prof.ev && h->tune_reps == 0;
+  const PatchBuf bufs[2] = {{in, pp * 4, false}, {out, pp * 4, true}};
   for (int s = 0; s < n; s += h->chunk) {
     const int m = std::min(h->chunk, n - s);
-    int rc = run_chunk(h, m, split, [&](Lane& ln, int o, int k) {
+    int rc = run_chunk(h, s, m, split, bufs, 2, [&](Lane& ln, int o, int k) {
       const int b = s + o;
       return run_layers(h, ln, 0, (int)h->layers.size(), in + b * pp, k, nullptr, nullptr, nullptr, out + b * pp,
                         prof);
@@ -1159,9 +1233,14 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
   h->s1_form = default_s1_form();
+  {
+    const StructDefaults sd = struct_defaults(model_id);
+    h->fuse01 = sd.fuse01;
+    h->fuse_tail = sd.fuse_tail;
+    h->chain = sd.chain;
+  }
   if (const char* f = getenv("TIC_FUSE01")) h->fuse01 = atoi(f) != 0;
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
-  else h->fuse_tail = kFuseTailDefault;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = atoi(f) == 1 ? 1 : 2;
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
@@ -1377,7 +1456,7 @@ int tic_memcpy_d2h(tic_handle* h, void* dst, const void* src, size_t bytes) {
   touch(h);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  return TIC_OK;
+  return check_chain_error(h);  // a timed-out chain hand-off made these bytes invalid
 }
 
 int tic_synchronize(tic_handle* h) {
@@ -1487,12 +1566,15 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
   }
   if (k == "chunk") {
     if (value < 1) return fail(TIC_EINVAL, "chunk must be >= 1");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);  // the chain's geometry check depends on the chunk
     h->chunk = value;
     return TIC_OK;
   }
-  if (k == "fuse01") {
+  if (k == "fuse01") {  // -1: the model's default
+    HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
-    h->fuse01 = value != 0;
+    h->fuse01 = value < 0 ? struct_defaults(h->model_id).fuse01 : value != 0;
     return TIC_OK;
   }
   if (k == "persist_grid") {
@@ -1508,7 +1590,7 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
   if (k == "fuse_tail") {
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
-    h->fuse_tail = value != 0;
+    h->fuse_tail = value < 0 ? struct_defaults(h->model_id).fuse_tail : value != 0;
     return TIC_OK;
   }
   if (k == "decouple") {  // lanes fork from the handle stream only when it has new work
@@ -1520,7 +1602,7 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
   if (k == "chain") {  // stride-1 runs in one wino_chain_kernel launch (Winograd form only)
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
-    h->chain = value != 0;
+    h->chain = value < 0 ? struct_defaults(h->model_id).chain : value != 0;
     return TIC_OK;
   }
   if (k == "chain_wh") {  // wino_chain_kernel workgroup: 1 = 256 threads, 2 = 512 threads
@@ -2065,8 +2147,16 @@ int tic_tuning_import(tic_handle* h, const char* text) {
         return fail(TIC_EINVAL, "tuning line %d: kernel does not match layer %s", line, ld.name.c_str());
       tuned[a][b] = ce;
     } else if (!strcmp(kind, "var")) {
-      if (sscanf(ln.c_str(), "var %d %d %d", &a, &b, &c) != 3 || a < 0 || a >= L || c < 0 || c >= 64)
+      if (sscanf(ln.c_str(), "var %d %d %d", &a, &b, &c) != 3 || a < 0 || a >= L || c < 0 || b == 0)
         return fail(TIC_EINVAL, "tuning line %d: bad var entry", line);
+      // the variant set of the layer's role: enc01 (layer 0, key -n), first layer (0, n),
+      // dec10 (layer L-2, n), last layer (L-1, n)
+      int nvar = -1;
+      if (a == 0) nvar = b < 0 ? tic::enc01_variants() : tic::rgb_in_variants();
+      else if (a == L - 1 && b > 0) nvar = tic::rgb_out_variants();
+      else if (a == L - 2 && b > 0) nvar = tic::dec10_variants();
+      if (c >= nvar)
+        return fail(TIC_EINVAL, "tuning line %d: variant %d is not a variant of layer %d (key %d)", line, c, a, b);
       vars[a][b] = c;
     } else {
       return fail(TIC_EINVAL, "tuning line %d: unknown entry %s", line, kind);

@@ -34,6 +34,7 @@ class ImageCodec:
         self.post = post
         self._bufs: dict[str, DeviceBuffer] = {}
         self._slot = 0
+        self.last_slot = 0  # event slot of the last post-filtered image (decode_image_device)
 
     # ------------------------------------------------------------------ geometry
     def grid(self, H: int, W: int) -> tuple[int, int]:
@@ -66,13 +67,20 @@ class ImageCodec:
 
     def decode_image_device(self, d_sym: DeviceBuffer, H: int, W: int, d_out: DeviceBuffer,
                             post_filter: bool = True) -> None:
-        """symbols (device) -> uint8 HWC image [H, W, 3] (device)."""
+        """symbols (device) -> uint8 HWC image [H, W, 3] (device).
+
+        Readiness of ``d_out``: with the post-filter it is written on the rmbe handle's
+        stream (so the next image's codec work is not held behind this image's filter);
+        it is complete after ``synchronize()``, or for stream-ordered consumers after
+        ``consumer.wait_event(self.post, slot)`` with the slot this call recorded
+        (``last_slot``).  Without the post-filter it is written on the codec's stream."""
         P = self.codec.patch_size
         n = self.num_patches(H, W)
         d_f = self._buf("patches_f32", n * P * P * 3 * 4)
         if post_filter and self.post is not None:
             k = self._slot
             self._slot = (k + 1) % self.NSLOT
+            self.last_slot = k
             d_img = self._buf(f"image_f32_{k}", H * W * 3 * 4)
             self.codec.decode_device(d_sym, n, None, d_f)
             # the rmbe pass that last filtered this stitch buffer (and wrote the previous

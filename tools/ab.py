@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--cfg", action="append", required=True, help="k=v[,k=v] codec options; env:KEY=V for env")
-    ap.add_argument("--tune-file", default=None, help="replay this tools/tune/*.json state instead of tuning")
+    ap.add_argument("--tune-file", default=None, help="replay this tf_image_compression_amd/tune/*.json state instead of tuning")
     ap.add_argument("--refork", action="store_true", help="every round starts from a fresh fork of the lanes")
     args = ap.parse_args()
     from tf_image_compression_amd.codec import Codec

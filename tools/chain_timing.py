@@ -7,7 +7,7 @@ phase boundaries (wino_chain.h, CH_TS), and tic_synchronize appends the last lau
 stamps to a file.  Prints, per chain launch (lane, encoder/decoder side), the spread of
 workgroup start times and the median / 90th-percentile duration of every phase per layer.
 
-    python tools/chain_timing.py [--tune-file tools/tune/model0_p256_b64_s2.json] [--steps 20] [--enc01]
+    python tools/chain_timing.py [--tune-file tf_image_compression_amd/tune/model0_p256_b64_s2.json] [--steps 20] [--enc01]
 """
 import argparse
 import json
@@ -75,7 +75,7 @@ def summarise_enc01(t):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tune-file", default=os.path.join(ROOT, "tools", "tune", "model0_p256_b64_s2.json"))
+    ap.add_argument("--tune-file", default=os.path.join(ROOT, "tf_image_compression_amd", "tune", "model0_p256_b64_s2.json"))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--enc01", action="store_true")

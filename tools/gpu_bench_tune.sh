@@ -1,6 +1,6 @@
 #!/bin/bash
 # Tune + bench model_0 (configs[1]) at 2 lanes with the step tuner's log (the tuned state
-# lands in gpurun_out/ for tools/tune/), then an alternating A/B replaying that state with
+# lands in gpurun_out/ for tf_image_compression_amd/tune/), then an alternating A/B replaying that state with
 # the chain off / on.
 set -e
 mkdir -p gpurun_out

@@ -3,7 +3,7 @@
 # chain off / on (512- and 256-thread workgroups) and one lane with the chain.
 set -e
 mkdir -p gpurun_out
-T=tools/tune/model0_p256_b64_s2.json
+T=tf_image_compression_amd/tune/model0_p256_b64_s2.json
 timeout -k 10 400 python -u tools/ab.py --model 0 --batch 64 --rounds 12 --steps 40 --tune-file $T --refork \
   --cfg streams=2,chain=0 \
   --cfg streams=2,chain=1,chain_wh=2 \
