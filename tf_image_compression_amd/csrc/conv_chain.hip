@@ -1,6 +1,6 @@
 // Chains of stride-1 64->64 layers in one launch (wino_chain.h): the codecs' residual
 // stages with their neighbouring stride-1 layers (model_0/model.py:98-144,148-196).
-#include "wino_chain.h"
+#include "wino_chain_cs.h"
 
 namespace tic {
 
@@ -18,8 +18,23 @@ static bool launch_wh(int in_mode, int out_mode, const ChainArgs& a, hipStream_t
   return true;
 }
 
+// channel-split shape (wino_chain_cs.h): two 256-thread workgroups per region
+static bool launch_cs(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s) {
+  const dim3 grid(a.n * a.rh * a.rw * 2), block(256);
+  if (in_mode == IN_F32 && out_mode == OUT_F32)
+    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_F32, OUT_F32>), grid, block, 0, s, a);
+  else if (in_mode == IN_F32 && out_mode == OUT_QUANT)
+    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_F32, OUT_QUANT>), grid, block, 0, s, a);
+  else if (in_mode == IN_IDX && out_mode == OUT_F32)
+    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_IDX, OUT_F32>), grid, block, 0, s, a);
+  else
+    return false;
+  return true;
+}
+
 bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh) {
   if (a.nl < 2 || a.nl > CH_MAX_LAYERS) return false;
+  if (wh == 3) return launch_cs(in_mode, out_mode, a, s);
   if (wh == 2) return launch_wh<2>(in_mode, out_mode, a, s);
   if (wh == 1) return launch_wh<1>(in_mode, out_mode, a, s);
   return false;
