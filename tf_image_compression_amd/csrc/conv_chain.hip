@@ -18,15 +18,16 @@ static bool launch_wh(int in_mode, int out_mode, const ChainArgs& a, hipStream_t
   return true;
 }
 
-// channel-split shape (wino_chain_cs.h): two 256-thread workgroups per region
+// channel-split shapes (wino_chain_cs.h): two workgroups per region, 256 or 512 threads
+template <int WH>
 static bool launch_cs(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s) {
-  const dim3 grid(a.n * a.rh * a.rw * 2), block(256);
+  const dim3 grid(a.n * a.rh * a.rw * 2), block(256 * WH);
   if (in_mode == IN_F32 && out_mode == OUT_F32)
-    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_F32, OUT_F32>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_F32, OUT_F32, WH>), grid, block, 0, s, a);
   else if (in_mode == IN_F32 && out_mode == OUT_QUANT)
-    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_F32, OUT_QUANT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_F32, OUT_QUANT, WH>), grid, block, 0, s, a);
   else if (in_mode == IN_IDX && out_mode == OUT_F32)
-    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_IDX, OUT_F32>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((wino_chain_cs_kernel<IN_IDX, OUT_F32, WH>), grid, block, 0, s, a);
   else
     return false;
   return true;
@@ -34,7 +35,8 @@ static bool launch_cs(int in_mode, int out_mode, const ChainArgs& a, hipStream_t
 
 bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh) {
   if (a.nl < 2 || a.nl > CH_MAX_LAYERS) return false;
-  if (wh == 3) return launch_cs(in_mode, out_mode, a, s);
+  if (wh == 3) return launch_cs<1>(in_mode, out_mode, a, s);
+  if (wh == 4) return launch_cs<2>(in_mode, out_mode, a, s);
   if (wh == 2) return launch_wh<2>(in_mode, out_mode, a, s);
   if (wh == 1) return launch_wh<1>(in_mode, out_mode, a, s);
   return false;

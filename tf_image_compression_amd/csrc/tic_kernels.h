@@ -119,8 +119,8 @@ bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int 
 // wino_chain.h; false if the mode combination is not compiled.
 struct ChainArgs;
 // wh: 1 = 256-thread workgroups, 2 = 512-thread workgroups (output channels split in halves
-// over the waves), 3 = two 256-thread workgroups per region (output channels split in halves
-// over the workgroups: wino_chain_cs.h)
+// over the waves), 3 / 4 = two 256- / 512-thread workgroups per region (output channels split
+// in halves over the workgroups: wino_chain_cs.h)
 bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh);
 
 // Whole-image glue and the symbol histogram (image_ops.hip).

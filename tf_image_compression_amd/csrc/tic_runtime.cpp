@@ -679,8 +679,8 @@ static int chain_end(const tic_handle* h, int li) {
   // byte offsets (n * R * 8 KB, n <= chunk) must fit the 32-bit buffer-resource range.
   {
     const int rw = (h->layers[li].h_in + 7) / 8;
-    const int per_region = h->chain_wh == 3 ? 2 : 1;  // workgroups per region
-    const long slots = (long)h->num_cus * (h->chain_wh == 2 ? 1 : 2);
+    const int per_region = h->chain_wh >= 3 ? 2 : 1;  // workgroups per region
+    const long slots = (long)h->num_cus * (h->chain_wh == 2 || h->chain_wh == 4 ? 1 : 2);
     if ((long)h->nlanes * per_region * (2L * rw + 2) > slots) return li;
     if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
   }
@@ -864,7 +864,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.ctl = ln.ctl;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
-        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R * (h->chain_wh == 3 ? 2 : 1), st, &a.tstamp);
+        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R * (h->chain_wh >= 3 ? 2 : 1), st, &a.tstamp);
         if (rc2) return rc2;
       }
       if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
@@ -1245,7 +1245,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE01")) h->fuse01 = atoi(f) != 0;
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
-  if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(3, std::max(1, atoi(f)));
+  if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(4, std::max(1, atoi(f)));
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) {
@@ -1608,8 +1608,8 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->chain = value < 0 ? struct_defaults(h->model_id).chain : value != 0;
     return TIC_OK;
   }
-  if (k == "chain_wh") {  // chain workgroup: 1 = 256 threads, 2 = 512, 3 = two 256-thread halves per region
-    if (value < 1 || value > 3) return fail(TIC_EINVAL, "chain_wh must be 1, 2 or 3");
+  if (k == "chain_wh") {  // chain workgroup: 1 = 256 threads, 2 = 512, 3 / 4 = two 256- / 512-thread halves per region
+    if (value < 1 || value > 4) return fail(TIC_EINVAL, "chain_wh must be 1..4");
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->chain_wh = value;
@@ -1884,7 +1884,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   if (!rc && h->chain && any_chain(h) && !getenv("TIC_CHAIN_WH")) {  // the chain's workgroup shape
     const int was = h->chain_wh;
     int best_wh = was;
-    for (int wh = 1; wh <= 3 && !rc; ++wh) {
+    for (int wh = 1; wh <= 4 && !rc; ++wh) {
       if (wh == was) continue;
       h->chain_wh = wh;
       clear_graphs(h);
@@ -2032,8 +2032,9 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     if (cs == i) {
       const int ce = chain_end(h, cs);
       const bool first_dec = !h->rmbe() && cs == h->n_enc, last_enc = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      if (h->chain_wh == 3)
-        snprintf(buf, sizeof buf, "wino_chain_cs_kernel<%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0);
+      if (h->chain_wh >= 3)
+        snprintf(buf, sizeof buf, "wino_chain_cs_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0,
+                 h->chain_wh - 2);
       else
         snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh);
     }
@@ -2144,7 +2145,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
       else if (!strcmp(name, "s1_form") && (a == 0 || a == 1)) s1_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
-      else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 3) chain_wh = a;
+      else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 4) chain_wh = a;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
     } else if (!strcmp(kind, "conv")) {
       if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)

@@ -37,18 +37,22 @@ constexpr int CH = 32;              // output channels per workgroup
 constexpr int XS = CH + 8;          // T-exchange pitch (== 8 mod 16)
 constexpr int XCH = 8 * NT * XS;    // [4 xi][2 b][16 tiles][XS] floats
 constexpr int HALF_FLOATS = 64 * CH;  // one region half's published interior: 8x8 px x 32 ch
-constexpr int NTH = 256;
 }  // namespace chcs
 
-template <int IN, int OUT>
-__global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a) {
+// WH: waves per transform-point row — 1: 256 threads, wave xi computes both 16-channel
+// blocks of the half; 2: 512 threads, waves xi and xi + 4 take one block each (two waves per
+// SIMD hide each other's LDS / L2 latency; per-output order unchanged, bit-identical).
+template <int IN, int OUT, int WH = 1>
+__global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_cs_kernel(const ChainArgs a) {
   using namespace chcs;
   using chain::tpix;
+  constexpr int NTH = 256 * WH;
   __shared__ __attribute__((aligned(16))) float smem[2 * TILE + XCH];
   __shared__ __attribute__((aligned(16))) float sbias[CH_MAX_LAYERS * C];
   __shared__ unsigned sh[2];
   const int tid = threadIdx.x;
-  const int xi = __builtin_amdgcn_readfirstlane(tid >> 6);  // point row of this wave
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int xi = wv & 3, wh = wv >> 2;  // point row, 16-channel block part (WH = 2)
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
   const int H = a.H, W = a.W, R = a.rh * a.rw, nR = a.n * R;
   auto stamp = [&](int k) {
@@ -70,12 +74,12 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
   const int cbase = half * CH;  // first output channel of this workgroup
 
   // ---- this half's weights of layer l, step s = 4 kc + nu, from L2, PF steps ahead ----
-  constexpr int NSTEP = 4 * KC, PF = 3, NBW = 2;
+  constexpr int NSTEP = 4 * KC, PF = 3, NBW = 2 / WH;
   f32x4 av[PF + 1][NBW];
   auto wglob = [&](int l, int s, int nb) -> f32x4 {
     const int kc = s >> 2, nu = s & 3;
     const float* wl = a.layer[l].wu + (size_t)xi * 64 * KC * C + (size_t)(lg * C + li) * 4;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * C + (2 * half + nb) * 64);
+    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * C + (2 * half + wh * NBW + nb) * 64);
   };
 #pragma unroll
   for (int p = 0; p < PF; ++p)
@@ -127,8 +131,10 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
   const int ty_l = li / TTX, tx_l = li % TTX;
   const int offA = ((2 * ty_l + iA) * RP + tx_l) * PS + lg * 4;
   const int offB = ((2 * ty_l + iB) * RP + tx_l) * PS + lg * 4;
-  // epilogue ownership: tile et, channel quad eq of this half, output row ay
-  const int et = (tid & 127) >> 3, eq = tid & 7, ay = tid >> 7;
+  // epilogue ownership: tile et, channel quad eq of this half, output row ay, and (WH = 2)
+  // output column b0 (WH = 1: both columns)
+  const int et = (tid & 127) >> 3, eq = tid & 7, ay = (tid >> 7) & 1, b0 = WH == 1 ? 0 : tid >> 8;
+  constexpr int NBC = 2 / WH;  // output columns per thread
   const int ety = et / TTX, etx = et % TTX;
   const int co = cbase + 4 * eq;
   float* const xch = smem + 2 * TILE;
@@ -202,7 +208,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const f32x4 m0 = acc[0][nb], m1 = acc[1][nb], m2 = acc[2][nb], m3 = acc[3][nb];
-      float* x = &xch[(xi * 2 * NT + li) * XS + nb * 16 + lg * 4];
+      float* x = &xch[(xi * 2 * NT + li) * XS + (wh * NBW + nb) * 16 + lg * 4];
       *reinterpret_cast<f32x4*>(x) = (m0 + m1) + m2;
       *reinterpret_cast<f32x4*>(x + NT * XS) = (m1 - m2) - m3;
     }
@@ -211,9 +217,10 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
     // ---- Y = A^T T for (tile et, quad eq, row ay), + bias, act, + residual ----
     const f32x4 bb = *reinterpret_cast<const f32x4*>(&sbias[l * C + co]);
     const bool relu = a.layer[l].act == ACT_RELU;
-    f32x4 y[2];
+    f32x4 y[NBC];
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+    for (int bi = 0; bi < NBC; ++bi) {
+      const int b = b0 + bi;
       f32x4 t[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
@@ -236,16 +243,16 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
         v.z = __fadd_rn(v.z, rr.z);
         v.w = __fadd_rn(v.w, rr.w);
       }
-      y[b] = v;
+      y[bi] = v;
     }
 
     if (last) {  // ---- the chain's output: global f32 or the quantiser, this half's channels ----
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int oy = oy0 + 2 * ety + ay, ox = ox0 + 2 * etx + b;
+      for (int bi = 0; bi < NBC; ++bi) {
+        const int oy = oy0 + 2 * ety + ay, ox = ox0 + 2 * etx + b0 + bi;
         if (oy >= H || ox >= W) continue;
         const size_t o = ((size_t)(nimg * H + oy) * W + ox) * C + co;
-        const f32x4 v = y[b];
+        const f32x4 v = y[bi];
         if constexpr (OUT == OUT_F32) {
           *reinterpret_cast<f32x4*>(a.out + o) = v;
         } else {
@@ -263,10 +270,10 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
     // (dst's interior is read by no one in this layer: res layers read it only at their own
     // output pixel, which this thread alone reads and then overwrites)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int ly = 2 * ety + ay, lx = 2 * etx + b;
+    for (int bi = 0; bi < NBC; ++bi) {
+      const int ly = 2 * ety + ay, lx = 2 * etx + b0 + bi;
       const bool in_img = oy0 + ly < H && ox0 + lx < W;
-      *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[b] : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[bi] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();
     stamp(ts + 2);
@@ -277,7 +284,7 @@ __global__ void __launch_bounds__(256, 2) wino_chain_cs_kernel(const ChainArgs a
     {
       const __amdgpu_buffer_rsrc_t rpub = chain::xrsrc(xl + (size_t)gh * HALF_FLOATS, HALF_FLOATS * 4);
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
+      for (int k = 0; k < 512 / NTH; ++k) {
         const int e = k * NTH + tid, px = e >> 3, q = e & 7;
         chain::st_sc1_16(rpub, (px * CH + 4 * q) * 4,
                          *reinterpret_cast<const f32x4*>(&dst[tpix((px >> 3) + 1, (px & 7) + 1) + cbase + 4 * q]));

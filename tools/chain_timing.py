@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--enc01", action="store_true")
+    ap.add_argument("--chain-wh", type=int, default=0, help="chain workgroup shape (option chain_wh), 0: the tuning's")
     args = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "chain_ts.bin")
     os.environ["TIC_ENC01_TIMING" if args.enc01 else "TIC_CHAIN_TIMING"] = path
@@ -93,6 +94,8 @@ def main():
         c.tuning_import(json.load(f)["tuning"])
     if not args.enc01:
         c.set_option("chain", 1)
+        if args.chain_wh:
+            c.set_option("chain_wh", args.chain_wh)
     eh, ew, ec = bottleneck_shape(M, P)
     x = np.random.default_rng(1234).integers(0, 256, (B, P, P, 3), dtype=np.uint8)
     d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(B * eh * ew * ec), c.alloc(x.nbytes)
