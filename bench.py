@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--patch", type=int, default=256)
     ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--profile-passes", type=int, default=5,
+                    help="one-lane per-layer timing passes; the median picks the dominant launch")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
@@ -81,11 +83,20 @@ def parse():
         args.model = 3
     if args.images is None:
         args.images = 10000 if args.workload == "sharded" else 1
-    if args.traffic is None:
-        # committed PMC summaries exist per model (tools/pmc); none for models 1/2 -> None
-        name = {0: "traffic_model0.json", 3: "traffic_model3.json"}.get(args.model)
-        args.traffic = os.path.join(ROOT, "tools", "pmc", name) if name else ""
     return args
+
+
+def traffic_path(args, model, lane_b):
+    """roofline.traffic source: --traffic, else the committed PMC summary of this model at this
+    per-launch batch (tools/pmc/traffic_model{M}_lb{lane_b}.json), else the model's default one
+    (tools/pmc/traffic_model{M}.json; pmc_traffic rejects it when its lane batch differs)."""
+    if args.traffic is not None:
+        return args.traffic
+    for name in (f"traffic_model{model}_lb{lane_b}.json", f"traffic_model{model}.json"):
+        path = os.path.join(ROOT, "tools", "pmc", name)
+        if os.path.exists(path):
+            return path
+    return ""
 
 
 def kernel_groups(codec, model_id, P, ms, kernels=None):
@@ -363,15 +374,16 @@ def main():
         return pmc_steady(args, codec, d_in, d_idx, d_rgb, lane_b, M, P)
 
     # per-layer kernel timing, outside the timed region: HIP events around each launch on
-    # the lane's stream, one lane at the per-launch batch (lane_b) — picks the dominant
-    # launch group, whose launches the timed region then times in-step (below)
-    codec.profile_layers(d_in, lane_b, 2)  # first use of the one-lane path: allocations, caches
-    ms = codec.profile_layers(d_in, lane_b, args.profile_iters)
+    # the lane's stream, one lane at the per-launch batch (lane_b), each launch running alone
+    # (exclusive) — the median of --profile-passes passes; it picks the dominant launch group
+    # (the most one-lane time per step) and gives its roofline fraction; the same launches are
+    # also timed in-step (below) and reported beside it
+    ms = one_lane_ms(codec, d_in, lane_b, args)
     kernels = codec.layer_kernels(lane_b)
     groups, rows = kernel_groups(codec, M, P, ms, kernels)
     names = {lay.name: i for i, lay in enumerate(layer_table(M))}
-    # candidates for the dominant group: the four largest by one-lane time per step
-    cands = sorted(groups, key=lambda k: -groups[k]["ms"])[:4]
+    # candidates timed in-step: the four largest by one-lane time per step
+    cands = sorted(groups, key=lambda k: (-groups[k]["ms"], -groups[k]["flops"]))[:4]
     for _ in range(args.warmup):
         codec.codec_device(d_in, B, d_idx, d_rgb)
     codec.synchronize()
@@ -403,10 +415,7 @@ def main():
             in_step[k] = codec.mark_durations()
         codec.set_option("mark_layer", -1)
     in_step = {k: v for k, v in in_step.items() if len(v)}
-    if in_step:
-        dom_key = max(in_step, key=lambda k: float(np.mean(in_step[k])) * groups[k]["launches"])
-    else:
-        dom_key = cands[0]
+    dom_key = cands[0]  # the most one-lane time per step
     marks = in_step.get(dom_key, np.zeros(0))
     if args.trace_only:
         if rank == 0:
@@ -424,22 +433,25 @@ def main():
     gathered = comm.allgather_stats(st)
     summary = dist.combine(gathered)
 
-    # the dominant group's roofline from its launches' durations in the timed steps (both
-    # lanes running, as rocprofv3 --kernel-trace sees them); every group's from the
-    # one-lane per-layer timing in roofline_groups
+    # the dominant group's roofline from its one-lane (exclusive) launch duration: a
+    # kernel-quality figure; beside it the same launches timed in the steady two-lane steps
+    # (sharing the chip with the other lane, as rocprofv3 --kernel-trace sees them there)
     dom = dict(groups[dom_key])
-    solo_ms = dom["ms"] / dom["launches"]
-    if len(marks):
-        dom["ms"] = float(np.mean(marks)) * dom["launches"]
     roof, dom_ms, dom_flops, dom_bytes = roofline_of(dom, lane_b)
-    roof["timing"] = (f"HIP events around each of its {len(marks)} launches on the lane streams in "
-                      f"{n_in_step} two-lane steps run right after the timed region (mean)"
-                      if len(marks) else "one-lane per-layer events")
-    roof["ms_per_launch_one_lane"] = round(solo_ms, 5)
+    roof["timing"] = (f"one lane, each launch alone: HIP events per launch, median of {args.profile_passes} "
+                      f"passes x {args.profile_iters} iterations")
+    if len(marks):
+        di = dict(groups[dom_key])
+        di["ms"] = float(np.mean(marks)) * di["launches"]
+        ri, rmsi, _, _ = roofline_of(di, lane_b)
+        roof["ms_per_launch_in_step"] = round(rmsi, 5)
+        roof["frac_in_step"] = ri["frac"]
+        roof["timing_in_step"] = (f"HIP events around each of its {len(marks)} launches on the lane streams in "
+                                  f"{n_in_step} two-lane steps run right after the timed region (mean)")
     # HBM bytes per launch of the dominant kernel instance from the committed PMC summary
     # (tools/pmc_box.sh + tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
     dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
-    roof.update(pmc_traffic(args.traffic, launch_units(groups[dom_key]["layers"], kernels, names),
+    roof.update(pmc_traffic(traffic_path(args, M, lane_b), launch_units(groups[dom_key]["layers"], kernels, names),
                             {"model": M, "patch": P, "lane_batch": lane_b}))
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
     roof["kernel"] = "+".join(groups[dom_key]["layers"])
@@ -505,6 +517,14 @@ def main():
         print(json.dumps(out), flush=True)
     comm.close()
     codec.close()
+
+
+def one_lane_ms(codec, d_in, lane_b, args):
+    """Per-layer one-lane launch durations (ms): the median over args.profile_passes passes
+    of tic_profile_layers (args.profile_iters iterations each), after a warm pass."""
+    codec.profile_layers(d_in, lane_b, 2)  # first use of the one-lane path: allocations, caches
+    runs = [codec.profile_layers(d_in, lane_b, args.profile_iters) for _ in range(max(1, args.profile_passes))]
+    return np.median(np.stack(runs), axis=0)
 
 
 def tune_cache_path(args, M, P, B):
@@ -612,7 +632,7 @@ def main_sharded(args):
     st = shard.stats(args.steps, wall0, wall1)
     summary = dist.combine(comm.allgather_stats(st))
     # the one-lane roofline of the dominant launch group at the shard's batch (as configs[1])
-    ms = codec.profile_layers(shard.d_img, lane_b, args.profile_iters) if shard.n >= lane_b else None
+    ms = one_lane_ms(codec, shard.d_img, lane_b, args) if shard.n >= lane_b else None
     roof = None
     if ms is not None:
         kernels = codec.layer_kernels(lane_b)
@@ -623,7 +643,7 @@ def main_sharded(args):
         names = {lay.name: i for i, lay in enumerate(layer_table(M))}
         dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
         winograd_note(roof, dom_kernels, dom_flops, dom_ms)
-        roof.update(pmc_traffic(args.traffic, launch_units(groups[dom_key]["layers"], kernels, names),
+        roof.update(pmc_traffic(traffic_path(args, M, lane_b), launch_units(groups[dom_key]["layers"], kernels, names),
                                 {"model": M, "patch": P, "lane_batch": lane_b}))
         roof["kernel"] = "+".join(groups[dom_key]["layers"])
         roof["kernel_instance"] = dom_kernels
@@ -778,8 +798,8 @@ def main_image(args):
     summary = dist.combine(comm.allgather_stats(st))
 
     # per-layer HIP-event timing of both networks at their per-launch batch sizes
-    ms_c = codec.profile_layers(d_pat, lane_b, args.profile_iters)
-    ms_r = post.profile_layers(d_win, win_lane, args.profile_iters)
+    ms_c = one_lane_ms(codec, d_pat, lane_b, args)
+    ms_r = one_lane_ms(post, d_win, win_lane, args)
     groups, rows = kernel_groups(codec, M, P, ms_c, codec.layer_kernels(lane_b))
     rgroups, rrows = kernel_groups(post, RMBE_ID, 128, ms_r, post.layer_kernels(win_lane))
     # dominant = largest time per image: per-launch ms x launches per image
@@ -795,7 +815,7 @@ def main_image(args):
     dom_kernels = sorted({kern[idx[nm]] for nm in g["layers"]} - {""})
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
     # HBM bytes per launch: only from a PMC summary of this exact configuration
-    roof.update(pmc_traffic(args.traffic if dom_key[0] != "rmbe" else "", launch_units(g["layers"], kern, idx),
+    roof.update(pmc_traffic(traffic_path(args, net_id, lb), launch_units(g["layers"], kern, idx),
                             {"model": net_id, "patch": P if dom_key[0] != "rmbe" else 128, "lane_batch": lb}))
     roof["kernel_instance"] = dom_kernels
     roof["kernel"] = ("rmbe:" if dom_key[0] == "rmbe" else f"model_{M}:") + "+".join(g["layers"])
