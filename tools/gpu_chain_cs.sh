@@ -16,3 +16,5 @@ step ctime2_$TAG 200 python tools/chain_timing.py --streams 2 --chain-wh 3
 for wh in 2 3 4; do
   TIC_TUNE_LOG=1 TIC_CHAIN_WH=$wh step bench_wh${wh}_$TAG 600 python bench.py --tune-cache none --no-cpu-baseline
 done
+step etime1_$TAG 200 python tools/chain_timing.py --streams 1 --enc01
+step etime2_$TAG 200 python tools/chain_timing.py --streams 2 --enc01
