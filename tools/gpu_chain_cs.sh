@@ -8,7 +8,8 @@ cd $R
 mkdir -p gpurun_out/tune_$TAG
 source tools/gpu_steps.sh
 O=$R/gpurun_out
-step chaintest_$TAG 600 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_product.py -v --timeout 300 --timeout-method thread
+step chaintest_$TAG 600 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_product.py tests/test_gpu_parity.py -k "chain or product or fused_first or splits or golden" -v --timeout 300 --timeout-method thread
+step probe_e01_$TAG 300 python tools/layer_probe.py 0 32 TIC_ENC01_VARIANT=3 TIC_ENC01_VARIANT=5 TIC_ENC01_VARIANT=4
 step probe_$TAG 300 python tools/layer_probe.py 0 32 opt:chain_wh=2 opt:chain_wh=3 opt:chain_wh=4
 step ctime1_$TAG 200 python tools/chain_timing.py --streams 1 --chain-wh 3
 step ctime1b_$TAG 200 python tools/chain_timing.py --streams 1 --chain-wh 4
