@@ -1876,9 +1876,29 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     if (!can) continue;
     *f.v = !was;
     clear_graphs(h);
-    float alt = 0.f;
-    rc = measure(&alt);
-    if (log && !rc) fprintf(stderr, "tune-step %s=%d : %.2f us\n", f.name, (int)*f.v, 1e3f * alt);
+    float alt = 1e30f;
+    if (f.v == &h->chain && !was && !getenv("TIC_CHAIN_WH")) {
+      // switching the chain on: in each of its workgroup shapes (whether it pays depends on
+      // the shape: the channel-split ones double the workgroups of small stages)
+      const int wh0 = h->chain_wh;
+      int best_wh = wh0;
+      for (int wh = 1; wh <= 4 && !rc; ++wh) {
+        h->chain_wh = wh;
+        clear_graphs(h);
+        if (!any_chain(h)) continue;
+        float m = 0.f;
+        rc = measure(&m);
+        if (log && !rc) fprintf(stderr, "tune-step chain=1 chain_wh=%d : %.2f us\n", wh, 1e3f * m);
+        if (!rc && m < alt) {
+          alt = m;
+          best_wh = wh;
+        }
+      }
+      h->chain_wh = alt < cur ? best_wh : wh0;
+    } else {
+      rc = measure(&alt);
+      if (log && !rc) fprintf(stderr, "tune-step %s=%d : %.2f us\n", f.name, (int)*f.v, 1e3f * alt);
+    }
     if (!rc && alt < cur) cur = alt;
     else *f.v = was;
     clear_graphs(h);
