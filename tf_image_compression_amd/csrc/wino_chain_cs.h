@@ -12,7 +12,8 @@
 // same order, the same epilogue — so every output is bit-identical to the unfused launch.
 //
 // Hand-off per layer: each workgroup publishes its half of the region's new 8x8 interior
-// (8 KB, 16-byte write-through sc1 stores, drained, then a per-(layer, region, half) flag);
+// straight from the epilogue's registers (8 KB, 16-byte write-through sc1 stores, drained,
+// then a per-(layer, region, half) flag);
 // it then needs its partner's half of the interior (8 KB) and the 1-pixel halo ring in all
 // 64 channels from the neighbouring regions' halves (9 KB), read with 16-byte sc1 buffer
 // loads after polling those flags (MI355X_MICROARCH.md hand-off table, row 1).  Progress:
@@ -266,34 +267,29 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_cs_kerne
       break;
     }
 
-    // ---- this half of the next layer's tile interior (zero outside the image) ----
+    // ---- this half of the next layer's tile interior (zero outside the image), written to
+    // LDS and published from the same registers: 16-byte write-through stores of the region
+    // half's 8x8 x 32 channels, drained, then (after the barrier) the flag ----
     // (dst's interior is read by no one in this layer: res layers read it only at their own
     // output pixel, which this thread alone reads and then overwrites)
-#pragma unroll
-    for (int bi = 0; bi < NBC; ++bi) {
-      const int ly = 2 * ety + ay, lx = 2 * etx + b0 + bi;
-      const bool in_img = oy0 + ly < H && ox0 + lx < W;
-      *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[bi] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    __syncthreads();
-    stamp(ts + 2);
-
-    // ---- publish this half of the interior: 64 px x 8 quads, 2 chunks per thread ----
     const int gh = g * 2 + half;
     float* const xl = a.xbuf + (size_t)l * nR * 2 * HALF_FLOATS;  // this layer's slots
     {
       const __amdgpu_buffer_rsrc_t rpub = chain::xrsrc(xl + (size_t)gh * HALF_FLOATS, HALF_FLOATS * 4);
 #pragma unroll
-      for (int k = 0; k < 512 / NTH; ++k) {
-        const int e = k * NTH + tid, px = e >> 3, q = e & 7;
-        chain::st_sc1_16(rpub, (px * CH + 4 * q) * 4,
-                         *reinterpret_cast<const f32x4*>(&dst[tpix((px >> 3) + 1, (px & 7) + 1) + cbase + 4 * q]));
+      for (int bi = 0; bi < NBC; ++bi) {
+        const int ly = 2 * ety + ay, lx = 2 * etx + b0 + bi;
+        const bool in_img = oy0 + ly < H && ox0 + lx < W;
+        const f32x4 v = in_img ? y[bi] : f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = v;
+        chain::st_sc1_16(rpub, ((ly * 8 + lx) * CH + 4 * eq) * 4, v);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0)
         __hip_atomic_store(&a.flags[(size_t)l * nR * 2 + gh], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    stamp(ts + 2);
     stamp(ts + 3);
     // ---- wait for the partner half and both halves of the (up to 8) neighbours ----
     if (tid < 18) {
