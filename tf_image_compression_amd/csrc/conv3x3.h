@@ -725,6 +725,13 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   // interior u8 tiles: each thread unpacks 4-pixel groups (12 bytes) of the 68-pixel row
   // segments; their loads are issued first so they fly together with the table's
   constexpr int GPR = 17, NG = R0 * GPR, NGI = (NG + 255) / 256;
+  // the table's loads go out first (L2-resident): with in-order load returns, its LDS copy
+  // then waits only for them, not for the u8 rows behind them
+  float lutv[3];
+  if constexpr (U8) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lutv[i] = a.nlut[i * 256 + tid];
+  }
   uint32_t wpre[NGI][3];
   if constexpr (U8) {
     if (!edge) {
@@ -744,8 +751,10 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   }
   if (edge)
     for (int e = tid; e < 3 * RGBP; e += 256) rgb[e] = 0.f;
-  if constexpr (U8)  // the host's f32 table (tic_finalize), same values as (v - mean) / std here
-    for (int e = tid; e < 768; e += 256) lut[e] = a.nlut[e];
+  if constexpr (U8) {  // the host's f32 table (tic_finalize), same values as (v - mean) / std here
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lut[i * 256 + tid] = lutv[i];
+  }
   if (edge || U8) __syncthreads();
   stamp(1);
   if constexpr (U8) {

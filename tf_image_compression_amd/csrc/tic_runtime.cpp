@@ -402,6 +402,7 @@ struct tic_handle {
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
+  int chain_order = 0;     // 1: regions by blockIdx (dispatch order), 0: atomic ticket (option "chain_order")
   int mark_layer = -1;     // tic_mark_durations: time the launches starting at this layer
   // Lane scheduling: lanes join into `stream` after every call, but wait on it (fork) only
   // when something else was enqueued there since their last fork ("decouple"), so lane k's
@@ -864,6 +865,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.xbuf = ln.xbuf;
       a.flags = ln.cflags;
       a.ctl = ln.ctl;
+      a.dispatch_order = h->chain_order;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
         int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R * (h->chain_wh >= 3 ? 2 : 1), st, &a.tstamp);
@@ -1248,6 +1250,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(4, std::max(1, atoi(f)));
+  if (const char* f = getenv("TIC_CHAIN_ORDER")) h->chain_order = atoi(f) != 0;
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) {
@@ -1615,6 +1618,12 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->chain_wh = value;
+    return TIC_OK;
+  }
+  if (k == "chain_order") {  // 1: chain regions by blockIdx (dispatch order), 0: atomic ticket
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->chain_order = value != 0;
     return TIC_OK;
   }
   if (k == "s1_form") {  // 0 direct, 1 Winograd, -1 the default (TIC_S1_FORM or built-in)

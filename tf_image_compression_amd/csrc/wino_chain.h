@@ -60,6 +60,8 @@ struct ChainArgs {
   float* xbuf;          // border exchange [nl-1][n*R][4 sides][8 px][64] f32
   unsigned* flags;      // [nl-1][n*R] epoch flags
   unsigned* ctl;        // [0] ticket, [1] done count, [2] epoch, [3] error (poll timeout)
+  int dispatch_order;   // 1: a workgroup's region is its blockIdx.x (the hardware's in-order
+                        // dispatch); 0: an atomic ticket (order guaranteed whatever the dispatch)
   int probe;            // timing probes only (TIC_CHAIN_PROBE; results invalid unless 0):
                         // 1 = no hand-off at all, 2 = publish but do not wait / read
   unsigned long long* tstamp;  // phase timestamps (TIC_CHAIN_TIMING; results stay valid) or
@@ -124,7 +126,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   stamp(0);
 
   if (tid == 0) {
-    sh[0] = __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[0] = a.dispatch_order ? blockIdx.x : __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh[1] = __hip_atomic_load(&a.ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // every layer's bias, read by the epilogues from LDS

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_cs_kerne
   };
   stamp(0);
   if (tid == 0) {
-    sh[0] = __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[0] = a.dispatch_order ? blockIdx.x : __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh[1] = __hip_atomic_load(&a.ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (int e = tid; e < a.nl * C; e += NTH) sbias[e] = a.layer[e / C].bias[e % C];

@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--tune-file", default=os.path.join(ROOT, "tf_image_compression_amd", "tune", "model0_p256_b64_s2.json"))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=64, help="patches per call (one lane: the per-launch batch)")
     ap.add_argument("--enc01", action="store_true")
     ap.add_argument("--chain-wh", type=int, default=0, help="chain workgroup shape (option chain_wh), 0: the tuning's")
     args = ap.parse_args()
@@ -87,7 +88,7 @@ def main():
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
     from tf_image_compression_amd.topology import bottleneck_shape
-    P, B, M = 256, 64, 0
+    P, B, M = 256, args.batch, 0
     c = Codec(M, synthetic_params(M, seed=0), SYNTH_MEAN, SYNTH_STD, patch_size=P)
     c.set_option("streams", args.streams)
     with open(args.tune_file) as f:
