@@ -14,9 +14,9 @@
 // layer of the chain (16 Winograd tiles = one 16-tile MFMA block; wave xi owns the
 // transform points (xi, 0..3)); the region's 10x10 input tile (1-pixel halo) stays in LDS
 // from layer to layer.  Between layers a region needs its neighbours' border pixels: each
-// workgroup publishes its 32 border pixels (rows 0 and 7, columns 0 and 7; 8 KB) with
-// write-through (sc1) 16-byte buffer stores, drains them, and raises a per-(layer, region)
-// flag; the neighbours poll the flags with sc1 loads and read the halo with 16-byte sc1
+// workgroup publishes its 32 border pixels (rows 0 and 7, columns 0 and 7; 8 KB) straight
+// from its epilogue registers with write-through (sc1) 16-byte buffer stores, drains them, and
+// raises a per-(layer, region) flag; the neighbours poll the flags with sc1 loads and read the halo with 16-byte sc1
 // buffer loads
 // (MI355X_MICROARCH.md, valid hand-off form, row 1).  No redundant halo recomputation,
 // ~1 hand-off per layer instead of a kernel boundary + full activation round trip.
@@ -346,7 +346,12 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       break;
     }
 
-    // ---- into the next layer's tile (interior), zero outside the image ----
+    // ---- into the next layer's tile (interior), zero outside the image; a border pixel is
+    // published from the same registers (16-byte write-through stores into this region's 8 KB
+    // record: side 0 / 1 = rows 0 / 7, side 2 / 3 = columns 0 / 7; corners go to two sides) ----
+    const bool handoff = R > 1 && a.probe != 1;
+    const size_t g = (size_t)nimg * R + reg;
+    const __amdgpu_buffer_rsrc_t rpub = xrsrc(a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C), 4 * 8 * C * 4);
     if (xch == dst) __syncthreads();  // every thread has read its T from dst's space
 #pragma unroll
     for (int k = 0; k < nay; ++k)
@@ -354,25 +359,21 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       for (int b = 0; b < 2; ++b) {
         const int ly = 2 * ety + ay0 + k, lx = 2 * etx + b;
         const bool in_img = oy0 + ly < H && ox0 + lx < W;
-        *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = in_img ? y[k][b] : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 v = in_img ? y[k][b] : f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = v;
+        if (handoff) {
+          if (ly == 0) st_sc1_16(rpub, ((0 * 8 + lx) * C + co) * 4, v);
+          if (ly == 7) st_sc1_16(rpub, ((1 * 8 + lx) * C + co) * 4, v);
+          if (lx == 0) st_sc1_16(rpub, ((2 * 8 + ly) * C + co) * 4, v);
+          if (lx == 7) st_sc1_16(rpub, ((3 * 8 + ly) * C + co) * 4, v);
+        }
       }
+    if (handoff) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     stamp(ts + 2);
 
-    // ---- hand-off: publish this region's border, then read the neighbours' ----
-    if (R > 1 && a.probe != 1) {
-      const size_t g = (size_t)nimg * R + reg;
-      float* const xb = a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C);
-      const __amdgpu_buffer_rsrc_t rpub = xrsrc(xb, 4 * 8 * C * 4);  // this region's 8 KB border
-#pragma unroll
-      for (int k = 0; k < 512 / NTH; ++k) {  // 4 sides x 8 pixels x 16 quads = 512 chunks
-        const int e = k * NTH + tid;
-        const int side = e >> 7, px = (e >> 4) & 7, q = e & 15;
-        const int ly = side == 0 ? 0 : (side == 1 ? 7 : px), lx = side == 2 ? 0 : (side == 3 ? 7 : px);
-        st_sc1_16(rpub, ((side * 8 + px) * C + 4 * q) * 4, *reinterpret_cast<const f32x4*>(&dst[tpix(ly + 1, lx + 1) + 4 * q]));
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    // ---- hand-off: raise this region's flag, then read the neighbours' borders ----
+    if (handoff) {
       if (tid == 0) __hip_atomic_store(&a.flags[(size_t)l * nR + g], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       stamp(ts + 3);
       // wait for the (up to 8) neighbours' flags of this layer
