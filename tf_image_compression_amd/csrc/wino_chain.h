@@ -207,6 +207,38 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   const int ety = et / TTX, etx = et % TTX;
   bool failed = false;
 
+  // halo descriptors of this thread, the same for every layer: the LDS offset in the tile and
+  // the byte offset of the neighbour's border record entry inside a layer's hand-off buffer
+  // (-1: outside the image, zero)
+  constexpr int HK = (36 * 16 + NTH - 1) / NTH;
+  int hlds[HK], hsrc[HK];
+#pragma unroll
+  for (int k = 0; k < HK; ++k) {
+    const int e = k * NTH + tid;
+    hlds[k] = hsrc[k] = -1;
+    if (e < 36 * 16) {
+      const int hp = e >> 4, q = e & 15;
+      int hy, hx;
+      if (hp < 10) hy = -1, hx = hp - 1;
+      else if (hp < 20) hy = 8, hx = hp - 11;
+      else if (hp < 28) hy = hp - 20, hx = -1;
+      else hy = hp - 28, hx = 8;
+      hlds[k] = tpix(hy + 1, hx + 1) + 4 * q;
+      const int gy = oy0 + hy, gx = ox0 + hx;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
+        const int ny = hy & 7, nx = hx & 7;  // pixel inside the neighbour region
+        int side, idx;
+        if (hy < 0) side = 1, idx = nx;
+        else if (hy > 7) side = 0, idx = nx;
+        else if (hx < 0) side = 3, idx = ny;
+        else side = 2, idx = ny;
+        const int gn = nimg * R + nry * a.rw + nrx;
+        hsrc[k] = (gn * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q) * 4;
+      }
+    }
+  }
+
   for (int l = 0; l < a.nl; ++l) {
     const bool last = l == a.nl - 1;
     const bool res = a.layer[l].res != 0;
@@ -393,30 +425,16 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       }
       __syncthreads();
       stamp(ts + 4);
-      // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16 quads
+      // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16
+      // quads, from the descriptors computed once before the layer loop (all loads first)
       const __amdgpu_buffer_rsrc_t rlay = xrsrc(a.xbuf + (size_t)l * nR * (4 * 8 * C), (unsigned)nR * (4 * 8 * C * 4));
-      for (int e = tid; e < 36 * 16; e += NTH) {
-        const int hp = e >> 4, q = e & 15;
-        int hy, hx;
-        if (hp < 10) hy = -1, hx = hp - 1;
-        else if (hp < 20) hy = 8, hx = hp - 11;
-        else if (hp < 28) hy = hp - 20, hx = -1;
-        else hy = hp - 28, hx = 8;
-        const int gy = oy0 + hy, gx = ox0 + hx;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (a.probe == 0 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-          const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
-          const int ny = hy & 7, nx = hx & 7;  // pixel inside the neighbour region
-          int side, idx;
-          if (hy < 0) side = 1, idx = nx;
-          else if (hy > 7) side = 0, idx = nx;
-          else if (hx < 0) side = 3, idx = ny;
-          else side = 2, idx = ny;
-          const int gn = nimg * R + nry * a.rw + nrx;
-          v = ld_sc1_16(rlay, (gn * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q) * 4);
-        }
-        *reinterpret_cast<f32x4*>(&dst[tpix(hy + 1, hx + 1) + 4 * q]) = v;
-      }
+      f32x4 hv[HK];
+#pragma unroll
+      for (int k = 0; k < HK; ++k)
+        hv[k] = hsrc[k] >= 0 && a.probe == 0 ? ld_sc1_16(rlay, hsrc[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < HK; ++k)
+        if (hlds[k] >= 0) *reinterpret_cast<f32x4*>(&dst[hlds[k]]) = hv[k];
       __syncthreads();
       stamp(ts + 5);
     } else {

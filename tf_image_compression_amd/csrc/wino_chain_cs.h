@@ -141,6 +141,39 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_cs_kerne
   float* const xch = smem + 2 * TILE;
   bool failed = false;
 
+  // read descriptors of this thread, the same for every layer: the partner's half of the
+  // interior (512 chunks), then the halo ring in all 64 channels (576); LDS offset in the tile
+  // and byte offset inside a layer's hand-off buffer (-1: outside the image, zero)
+  constexpr int NPART = 64 * (CH / 4), NHALO = 36 * 16;
+  constexpr int NLD = (NPART + NHALO + NTH - 1) / NTH;
+  int rlds[NLD], rsrc[NLD];
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int e = k * NTH + tid;
+    rlds[k] = rsrc[k] = -1;
+    if (e < NPART) {
+      const int px = e >> 3, q = e & 7;
+      const int oh = 1 - half;
+      rsrc[k] = (((g * 2 + oh) * 64 + px) * CH + 4 * q) * 4;
+      rlds[k] = tpix((px >> 3) + 1, (px & 7) + 1) + oh * CH + 4 * q;
+    } else if (e < NPART + NHALO) {
+      const int hpq = e - NPART, hp = hpq >> 4, q = hpq & 15;
+      int hy, hx;
+      if (hp < 10) hy = -1, hx = hp - 1;
+      else if (hp < 20) hy = 8, hx = hp - 11;
+      else if (hp < 28) hy = hp - 20, hx = -1;
+      else hy = hp - 28, hx = 8;
+      rlds[k] = tpix(hy + 1, hx + 1) + 4 * q;
+      const int gy = oy0 + hy, gx = ox0 + hx;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
+        const int npx = (hy & 7) * 8 + (hx & 7);  // pixel inside the neighbour region
+        const int gn = nimg * R + nry * a.rw + nrx;
+        rsrc[k] = (((gn * 2 + (q >> 3)) * 64 + npx) * CH + 4 * (q & 7)) * 4;
+      }
+    }
+  }
+
   for (int l = 0; l < a.nl; ++l) {
     const bool last = l == a.nl - 1;
     const bool res = a.layer[l].res != 0;
@@ -309,44 +342,16 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_cs_kerne
     }
     __syncthreads();
     stamp(ts + 4);
-    // ---- read the partner's half of the interior and the halo ring (all 64 channels) ----
+    // ---- read the partner's half of the interior and the halo ring (all 64 channels), from
+    // the descriptors computed once before the layer loop (all loads first) ----
     {
       const __amdgpu_buffer_rsrc_t rlay = chain::xrsrc(xl, (unsigned)nR * 2 * HALF_FLOATS * 4);
-      constexpr int NPART = 64 * (CH / 4);  // 512 chunks
-      constexpr int NHALO = 36 * 16;        // 576 chunks
-      constexpr int NLD = (NPART + NHALO + NTH - 1) / NTH;
       f32x4 v[NLD];
-      int lds[NLD];
 #pragma unroll
-      for (int k = 0; k < NLD; ++k) {
-        const int e = k * NTH + tid;
-        v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        lds[k] = -1;
-        if (e < NPART) {
-          const int px = e >> 3, q = e & 7;
-          const int oh = 1 - half;
-          v[k] = chain::ld_sc1_16(rlay, (((g * 2 + oh) * 64 + px) * CH + 4 * q) * 4);
-          lds[k] = tpix((px >> 3) + 1, (px & 7) + 1) + oh * CH + 4 * q;
-        } else if (e < NPART + NHALO) {
-          const int hpq = e - NPART, hp = hpq >> 4, q = hpq & 15;
-          int hy, hx;
-          if (hp < 10) hy = -1, hx = hp - 1;
-          else if (hp < 20) hy = 8, hx = hp - 11;
-          else if (hp < 28) hy = hp - 20, hx = -1;
-          else hy = hp - 28, hx = 8;
-          lds[k] = tpix(hy + 1, hx + 1) + 4 * q;
-          const int gy = oy0 + hy, gx = ox0 + hx;
-          if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-            const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
-            const int npx = (hy & 7) * 8 + (hx & 7);  // pixel inside the neighbour region
-            const int gn = nimg * R + nry * a.rw + nrx;
-            v[k] = chain::ld_sc1_16(rlay, (((gn * 2 + (q >> 3)) * 64 + npx) * CH + 4 * (q & 7)) * 4);
-          }
-        }
-      }
+      for (int k = 0; k < NLD; ++k) v[k] = rsrc[k] >= 0 ? chain::ld_sc1_16(rlay, rsrc[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < NLD; ++k)
-        if (lds[k] >= 0) *reinterpret_cast<f32x4*>(&dst[lds[k]]) = v[k];
+        if (rlds[k] >= 0) *reinterpret_cast<f32x4*>(&dst[rlds[k]]) = v[k];
     }
     __syncthreads();
     stamp(ts + 5);
