@@ -2085,6 +2085,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
       static const int th1[5] = {2, 4, 2, 4, 8};
       if (v == 5)
         snprintf(buf, sizeof buf, "enc01p_kernel<%d,%d,4,%s>", d.cout, h->layers[1].def.cout, tf[!h->rmbe()]);
+      else if (v == 6)
+        snprintf(buf, sizeof buf, "enc01pc_kernel<%d,%d,%s>", d.cout, h->layers[1].def.cout, tf[!h->rmbe()]);
       else
         snprintf(buf, sizeof buf, "enc01_kernel<%d,%d,%d,%s,%s>", d.cout, h->layers[1].def.cout, th1[v % 5],
                  tf[!h->rmbe()], tf[v >= 2]);
