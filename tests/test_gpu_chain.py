@@ -118,7 +118,7 @@ def test_wino_chain_device_path_and_tuning_replay():
             with pytest.raises(ValueError):
                 c2.tuning_import("tic-tuning 1\nconv 0 8 2 0\n")  # a T2 kernel for the first layer
             # variants are validated against the layer role's variant set
-            for bad in ("var 5 32 1", "var 0 -32 7", "var 0 32 3", "var 16 32 16", "var 17 32 12", "var 16 -32 1"):
+            for bad in ("var 5 32 1", "var 0 -32 5", "var 0 32 3", "var 16 32 16", "var 17 32 12", "var 16 -32 1"):
                 with pytest.raises(ValueError):
                     c2.tuning_import("tic-tuning 1\n" + bad + "\n")
             assert c2.tuning_export() == text  # nothing applied by the rejected imports

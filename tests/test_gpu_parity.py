@@ -259,7 +259,7 @@ def test_autotuned_equals_default(lib_codec):
         b.free()
 
 
-ENC01_VARIANTS = range(7)  # conv_rgb.hip enc01_variants(): TH1 2/4 padded, 2/4/8 compact, 4 persistent (5, 6)
+ENC01_VARIANTS = range(5)  # conv_rgb.hip enc01_variants(): TH1 2/4 padded, 2/4/8 compact
 
 
 @pytest.mark.parametrize("model_id,P", [(0, 256), (0, 48), (1, 64), (3, 128), (2, 64)])
@@ -274,13 +274,9 @@ def test_fused_first_layers_bit_identical(lib_codec, monkeypatch, model_id, P):
         codec.set_option("fuse01", 1)
         for v in ENC01_VARIANTS:
             monkeypatch.setenv("TIC_ENC01_VARIANT", str(v))
-            # the persistent variant (5) also with a grid of 7 workgroups, each walking many tiles
-            for cap in ((0, 7) if v >= 5 else (0,)):
-                codec.set_option("persist_grid", cap)
-                idx1, pre1 = codec.encode(x, return_preact=True)
-                assert np.array_equal(pre0, pre1) and np.array_equal(idx0, idx1), (v, cap)
+            idx1, pre1 = codec.encode(x, return_preact=True)
+            assert np.array_equal(pre0, pre1) and np.array_equal(idx0, idx1), v
     finally:
-        codec.set_option("persist_grid", 0)
         codec.set_option("fuse01", -1)
 
 
@@ -296,10 +292,7 @@ def test_fused_rmbe_first_layers_bit_identical(monkeypatch):
         c.set_option("fuse01", 1)
         for v in ENC01_VARIANTS:
             monkeypatch.setenv("TIC_ENC01_VARIANT", str(v))
-            for cap in ((0, 5) if v >= 5 else (0,)):
-                c.set_option("persist_grid", cap)
-                assert np.array_equal(a, c.rmbe_windows(win)), (v, cap)
-        c.set_option("persist_grid", 0)
+            assert np.array_equal(a, c.rmbe_windows(win)), v
 
 
 def test_quan_scale_256(lib_codec):

@@ -6,8 +6,6 @@
 #include "conv3x3.h"
 #include "convT_rgb_valu.h"
 #include "dec10.h"
-#include "enc01p.h"
-#include "enc01pc.h"
 
 namespace tic {
 
@@ -44,36 +42,10 @@ bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream
 // (TH 4/8/16), 6-11 VALU form (TW 64/32/16; 9-11 persistent, software-pipelined).  The form is a fixed policy (default VALU;
 // TIC_RGB_OUT_FORM=dense|scatter for experiments); tuning picks a tiling within the form,
 // so it never changes results.
-// TH1 = 2, 4 (padded LDS form), 2, 4, 8 (compact form), 5: TH1 = 4 persistent and
-// software-pipelined (enc01p.h), 6: TH1 = 4 persistent producer / consumer waves
-// (enc01pc.h) — all bit-identical
-int enc01_variants() { return 7; }
-
-template <int C0, int C1>
-static bool enc01_pc(bool u8_input, const Enc01Args& a, int n, hipStream_t s) {
-  constexpr int TH1 = 4;
-  const int ntx = (a.W2 + 15) / 16, nty = (a.H2 + TH1 - 1) / TH1, ntiles = ntx * nty * n;
-  int grid = std::min(ntiles, std::max(1, a.num_cus));
-  if (a.grid_cap > 0) grid = std::min(grid, a.grid_cap);
-  if (u8_input)
-    hipLaunchKernelGGL((enc01pc_kernel<C0, C1, true>), dim3(grid), dim3(512), 0, s, a, ntx, nty, ntiles);
-  else
-    hipLaunchKernelGGL((enc01pc_kernel<C0, C1, false>), dim3(grid), dim3(512), 0, s, a, ntx, nty, ntiles);
-  return true;
-}
-
-template <int C0, int C1>
-static bool enc01_persist(bool u8_input, const Enc01Args& a, int n, hipStream_t s) {
-  constexpr int TH1 = 4;
-  const int ntx = (a.W2 + 15) / 16, nty = (a.H2 + TH1 - 1) / TH1, ntiles = ntx * nty * n;
-  int grid = std::min(ntiles, 2 * std::max(1, a.num_cus));
-  if (a.grid_cap > 0) grid = std::min(grid, a.grid_cap);
-  if (u8_input)
-    hipLaunchKernelGGL((enc01p_kernel<C0, C1, TH1, true>), dim3(grid), dim3(256), 0, s, a, ntx, nty, ntiles);
-  else
-    hipLaunchKernelGGL((enc01p_kernel<C0, C1, TH1, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty, ntiles);
-  return true;
-}
+// TH1 = 2, 4 (padded LDS form), 2, 4, 8 (compact form) — all bit-identical.  (Round 3 measured
+// a persistent software-pipelined form and a producer / consumer form and did not keep them:
+// 59 and 75 against 50 us per 32 patches)
+int enc01_variants() { return 5; }
 
 template <int C0, int C1, int TH1, bool CMP>
 static bool enc01_th(bool u8_input, const Enc01Args& a, int n, hipStream_t s) {
@@ -93,8 +65,6 @@ static bool enc01_c(bool u8_input, const Enc01Args& a, int n, hipStream_t s, int
     case 2: return enc01_th<C0, C1, 2, true>(u8_input, a, n, s);
     case 3: return enc01_th<C0, C1, 4, true>(u8_input, a, n, s);
     case 4: return enc01_th<C0, C1, 8, true>(u8_input, a, n, s);
-    case 5: return enc01_persist<C0, C1>(u8_input, a, n, s);
-    case 6: return enc01_pc<C0, C1>(u8_input, a, n, s);
   }
   return false;
 }

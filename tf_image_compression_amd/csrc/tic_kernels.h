@@ -54,8 +54,6 @@ struct Enc01Args {
   float mean[3], std[3];
   const float* nlut;   // u8 input: [3][256] (v - mean[c]) / std[c] in f32, computed on the host
   unsigned long long* tstamp;  // phase timestamps (TIC_ENC01_TIMING) or null: [workgroup][8]
-  int num_cus;         // the persistent variant sizes its grid from it
-  int grid_cap;        // > 0: cap on the persistent grid (tests: several tiles per workgroup)
 };
 
 struct RgbOutArgs {
@@ -106,7 +104,7 @@ const ConvEntry* conv_registry_t2(int* count);
 // bit-identical.
 int rgb_in_variants();
 int enc01_variants();
-constexpr int kEnc01Default = 3;  // compact LDS form, 4 layer-1 rows (5: persistent, enc01p.h)
+constexpr int kEnc01Default = 3;  // compact LDS form, 4 layer-1 rows
 bool launch_enc01(int c0, int c1, bool u8_input, const Enc01Args& a, int n, hipStream_t s, int variant);
 int rgb_out_variants();
 bool launch_rgb_in(int cout, bool u8_input, const RgbInArgs& a, int n, hipStream_t s, int variant);

@@ -768,8 +768,6 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.pad0y = a.pad0x = same_pad(d.kind, lay.h_in);
       a.pad1y = a.pad1x = same_pad(K_S2, l1r.h_in);
       a.nlut = h->d_nlut;
-      a.num_cus = h->num_cus;
-      a.grid_cap = h->persist_grid;
       for (int c = 0; c < 3; ++c) {
         a.mean[c] = h->mean[c];
         a.std[c] = h->std[c];
@@ -2083,13 +2081,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
       int v = iv != l.tuned_var.end() ? iv->second : tic::kEnc01Default;
       if (const char* t = getenv("TIC_ENC01_VARIANT")) v = atoi(t);
       static const int th1[5] = {2, 4, 2, 4, 8};
-      if (v == 5)
-        snprintf(buf, sizeof buf, "enc01p_kernel<%d,%d,4,%s>", d.cout, h->layers[1].def.cout, tf[!h->rmbe()]);
-      else if (v == 6)
-        snprintf(buf, sizeof buf, "enc01pc_kernel<%d,%d,%s>", d.cout, h->layers[1].def.cout, tf[!h->rmbe()]);
-      else
-        snprintf(buf, sizeof buf, "enc01_kernel<%d,%d,%d,%s,%s>", d.cout, h->layers[1].def.cout, th1[v % 5],
-                 tf[!h->rmbe()], tf[v >= 2]);
+      snprintf(buf, sizeof buf, "enc01_kernel<%d,%d,%d,%s,%s>", d.cout, h->layers[1].def.cout, th1[v % 5],
+               tf[!h->rmbe()], tf[v >= 2]);
     }
   } else if (i == 0 || i == L - 1) {
     auto iv = l.tuned_var.find(n);
