@@ -37,6 +37,20 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// XCD-aware block order (MI355X_MICROARCH.md: blocks b and b + 8 are dealt to one XCD):
+// logical tile b' = (b % 8) * (N / 8) + b / 8, so each XCD walks a contiguous run of tiles —
+// x fastest, then the next tile row — and a tile's halo rows, which the tile above read a
+// moment earlier on the same XCD, come from that XCD's L2 instead of HBM.  Placement only:
+// every tile computes exactly what it did.  (N not a multiple of 8: identity.)
+__device__ __forceinline__ void xcd_tile(int& bx, int& by, int& bz) {
+  const unsigned gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+  unsigned b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if ((n & 7u) == 0) b = (b & 7u) * (n >> 3) + (b >> 3);
+  bx = (int)(b % gx);
+  by = (int)((b / gx) % gy);
+  bz = (int)(b / (gx * gy));
+}
+
 // Quantiser: round_half_even(sigmoid(v) * (Q-1)), clamped to [0, Q-1].
 __device__ __forceinline__ uint32_t quant1(float v, float qscale) {
   float s = 1.0f / (1.0f + expf(-v));

@@ -88,9 +88,11 @@ __global__ void __launch_bounds__(256) conv3x3_wino_kernel(const ConvArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[TILE > XCH ? TILE : XCH];
 
   const int tid = threadIdx.x;
-  const int split = NSPLIT > 1 ? (int)(blockIdx.x % NSPLIT) : 0;
-  const int bx = NSPLIT > 1 ? (int)(blockIdx.x / NSPLIT) : (int)blockIdx.x;
-  const int oy0 = blockIdx.y * (2 * TTY), ox0 = bx * (2 * TTX), nimg = blockIdx.z;
+  int lbx, lby, lbz;
+  xcd_tile(lbx, lby, lbz);
+  const int split = NSPLIT > 1 ? lbx % NSPLIT : 0;
+  const int bx = NSPLIT > 1 ? lbx / NSPLIT : lbx;
+  const int oy0 = lby * (2 * TTY), ox0 = bx * (2 * TTX), nimg = lbz;
   const int H = a.H, W = a.W;
   const int xi = __builtin_amdgcn_readfirstlane(tid >> 6);  // B^T row of this wave
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
