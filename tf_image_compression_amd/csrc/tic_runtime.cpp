@@ -1837,6 +1837,23 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     return h->rmbe() ? rmbe_dev(h, (const float*)d_in, n, (float*)d_out, Prof{nullptr})
                      : codec_dev(h, (const uint8_t*)d_in, n, (uint8_t*)d_idx, (uint8_t*)d_out);
   };
+  // a chain launch whose hand-off timed out (wino_chain_kernel's bounded poll: its regions
+  // could not all be scheduled) leaves the lane's error word set; a candidate that did so is
+  // rejected (measured as infinitely slow) and the word cleared, so tuning never leaves a
+  // stale error behind for the caller's next synchronisation
+  auto chain_failed = [&]() -> bool {
+    bool any = false;
+    for (Lane& ln : h->lanes) {
+      if (!ln.ctl) continue;
+      unsigned w = 0;
+      if (hipMemcpy(&w, ln.ctl + 3, sizeof w, hipMemcpyDeviceToHost) != hipSuccess) continue;
+      if (w) {
+        (void)hipMemset(ln.ctl + 3, 0, sizeof(unsigned));
+        any = true;
+      }
+    }
+    return any;
+  };
   auto measure = [&](float* best) -> int {
     *best = 1e30f;
     int r = step();  // warm
@@ -1855,6 +1872,10 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       float ms = 0.f;
       HIP_TRY(hipEventElapsedTime(&ms, t0, t1));
       *best = std::min(*best, ms / reps);
+    }
+    if (chain_failed()) {
+      if (getenv("TIC_TUNE_LOG")) fprintf(stderr, "tune-step: a chain hand-off timed out: candidate rejected\n");
+      *best = 1e30f;
     }
     return TIC_OK;
   };
