@@ -61,6 +61,18 @@ def test_codec_model3_256(m3_256):
     check_codec(codec, params, 3, 256, structured_patches(2, 256, seed=301))
 
 
+@pytest.mark.parametrize("form", [1, 2])
+def test_codec_model3_256_s1_form(m3_256, form):
+    """configs[2] geometry in each Winograd form of the residual stages (F(2x2,3x3) and
+    F(4x4,3x3)) against the oracle, 4 patches."""
+    codec, params = m3_256
+    try:
+        codec.set_option("s1_form", form)
+        check_codec(codec, params, 3, 256, structured_patches(4, 256, seed=307))
+    finally:
+        codec.set_option("s1_form", -1)
+
+
 def test_model3_256_batch_256_invariance(m3_256):
     """configs[2] batch: 256 patches in one call equal the same patches run 2 at a time
     (bit for bit, symbols and uint8), and a second run is identical (determinism)."""

@@ -164,13 +164,62 @@ def test_conv3x3_winograd(lib_codec, act, res, H, W):
         assert np.array_equal(got, outs[0][1]), tile
 
 
-@pytest.mark.parametrize("model_id,P", [(0, 64), (3, 64), (1, 32)])
+# Winograd F(4x4,3x3) tilings (th = 4 TTY: 4x64, 8x32, 16x16 output pixels per workgroup)
+WINO4_TILES = [4, 8, 16]
+
+
+@pytest.mark.parametrize("act,res,H,W", [(1, False, 16, 16), (1, True, 20, 13), (1, True, 64, 64),
+                                         (1, False, 7, 40), (1, False, 33, 17), (1, True, 32, 32)])
+def test_conv3x3_winograd4(lib_codec, act, res, H, W):
+    """Winograd F(4x4,3x3) form (conv3x3_wino4.h): within the per-layer bar of the oracle,
+    every tiling bit-identical to every other, partial tiles at odd sizes included, no
+    output left unwritten."""
+    import os
+    codec, _ = lib_codec(0, 64)
+    cin = cout = 64
+    r = np.random.default_rng(np.random.PCG64(4777 + H * 100 + W))
+    n = 3
+    x = r.standard_normal((n, H, W, cin)).astype(np.float32)
+    k = (r.standard_normal((3, 3, cin, cout)) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+    b = (r.standard_normal(cout) * 0.1).astype(np.float32)
+    ref = o.my_conv2d(x, {"l/kernel": k, "l/bias": b}, "l", 1, "relu" if act else "identity")
+    resid = r.standard_normal(ref.shape).astype(np.float32) if res else None
+    if res:
+        ref = ref + resid
+    d_in, d_out = codec.alloc(x.nbytes), codec.alloc(ref.nbytes)
+    d_in.upload(x)
+    d_res = None
+    if res:
+        d_res = codec.alloc(resid.nbytes)
+        d_res.upload(resid)
+    outs = []
+    try:
+        for th in WINO4_TILES:
+            os.environ["TIC_FORCE_TILE"] = f"{th},1,5,1"
+            d_out.upload(np.full(ref.shape, np.nan, np.float32))
+            codec.conv3x3_device(0, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
+            outs.append((th, d_out.download(ref.shape, np.float32)))
+    finally:
+        os.environ.pop("TIC_FORCE_TILE", None)
+    for buf in (d_in, d_out, d_res):
+        if buf is not None:
+            buf.free()
+    scale = max(1.0, float(np.max(np.abs(ref))))
+    for tile, got in outs:
+        assert not np.isnan(got).any(), tile
+        err = float(np.max(np.abs(got - ref)))
+        assert err <= 3e-5 * scale, (tile, err, scale)
+        assert np.array_equal(got, outs[0][1]), tile
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 64), (3, 64), (1, 32), (3, 128)])
 def test_codec_s1_forms(lib_codec, model_id, P):
-    """Both stride-1 forms (direct, Winograd) meet the end-to-end parity bar."""
+    """Every stride-1 form (direct, Winograd F(2x2,3x3), Winograd F(4x4,3x3) — layers with
+    no F(4x4,3x3) instance fall back to F(2x2,3x3)) meets the end-to-end parity bar."""
     codec, params = lib_codec(model_id, P)
     patches = structured_patches(2, P, seed=61 + model_id)
     try:
-        for form in (0, 1):
+        for form in (0, 1, 2):
             codec.set_option("s1_form", form)
             _check_codec(codec, params, model_id, P, patches)
     finally:

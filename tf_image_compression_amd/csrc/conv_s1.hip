@@ -1,9 +1,11 @@
 // Stride-1 'SAME' 3x3 convolutions: res_block convs (basic_block/basic_block.py:74-93),
 // encode_4 / decode_4 of model_0/1 (model_0/model.py:124-134,159-169), rmbe conv_3/4.
-// Two forms: the direct implicit GEMM (conv3x3_kernel, several tilings) and Winograd
-// F(2x2,3x3) (conv3x3_wino.h, weight source 4); the runtime picks the form by policy
+// Three forms: the direct implicit GEMM (conv3x3_kernel, several tilings), Winograd
+// F(2x2,3x3) (conv3x3_wino.h, weight source 4) and Winograd F(4x4,3x3) (conv3x3_wino4.h,
+// weight source 5, 64 -> 64 res-block convs); the runtime picks the form by policy
 // (option "s1_form") and a tiling within it by grid size or measurement (tic_runtime.cpp).
 #include "conv3x3_wino.h"
+#include "conv3x3_wino4.h"
 #include "conv_launch.h"
 
 #define S1_VARIANTS(ACT, RES, IN, OUT)                                 \
@@ -36,7 +38,15 @@
       TIC_WINO(CIN, COUT, 2, 1, 4, ACT, RES, IN, OUT),                 \
       TIC_WINO(CIN, COUT, 1, 1, 4, ACT, RES, IN, OUT)
 
+// Winograd F(4x4,3x3) tilings (TTY = 1, 2, 4 tile rows: 4x64, 8x32, 16x16 output pixels per
+// workgroup) for the 64 -> 64 res-block convs of model_3 and the rmbe net (form 2)
+#define S1_WINO4(ACT, RES, IN, OUT)                 \
+  TIC_WINO4(64, 64, 1, ACT, RES, IN, OUT),          \
+      TIC_WINO4(64, 64, 2, ACT, RES, IN, OUT),      \
+      TIC_WINO4(64, 64, 4, ACT, RES, IN, OUT)
+
 namespace tic {
+// new entries go at the end: tuning files name entries by their index in this table
 static const ConvEntry kS1[] = {
     S1_VARIANTS(ACT_RELU, false, IN_F32, OUT_F32),
     S1_VARIANTS(ACT_RELU, true, IN_F32, OUT_F32),
@@ -52,6 +62,8 @@ static const ConvEntry kS1[] = {
     S1_128(128, 128, ACT_RELU, true, IN_F32, OUT_F32),
     S1_128(128, 64, ACT_ID, false, IN_F32, OUT_QUANT),
     S1_128(64, 128, ACT_ID, false, IN_IDX, OUT_F32),
+    S1_WINO4(ACT_RELU, false, IN_F32, OUT_F32),
+    S1_WINO4(ACT_RELU, true, IN_F32, OUT_F32),
 };
 const ConvEntry* conv_registry_s1(int* count) {
   *count = sizeof(kS1) / sizeof(kS1[0]);

@@ -170,10 +170,22 @@ int same_pad(int kind, int h) {
 // workgroups.  `form` 1 selects the Winograd variants of stride-1 layers (weight source 4)
 // where compiled, 0 the direct ones.  TIC_FORCE_TILE="th,nsplit[,wsrc[,wr]]" overrides
 // (tuning experiments, tests); a forced weight source also overrides the form.
+// stride-1 form of a compiled entry: 1 Winograd F(2x2,3x3) (weight source 4), 2 Winograd
+// F(4x4,3x3) (weight source 5), else 0 (direct)
+int entry_form(const tic::ConvEntry& c) { return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : 0); }
+
 bool form_match(const tic::ConvEntry& c, int form, int fwl) {
   if (fwl >= 0) return c.wlds == fwl;
   if (c.wlds == 3) return false;  // persistent variants: only by autotune or forced
-  return (c.wlds == 4) == (form == 1);
+  return entry_form(c) == form;
+}
+
+// Forms tried for a layer whose policy is `form`, in order: a signature without an F(4x4,3x3)
+// instance runs F(2x2,3x3), one without Winograd instances the direct form.
+int form_fallback(int form, int pass) {
+  if (pass == 0) return form;
+  if (pass == 1) return form == 2 ? 1 : (form == 1 ? 0 : -1);
+  return form == 2 ? 0 : -1;
 }
 
 const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, int in, int outm, int hg = 0,
@@ -185,9 +197,9 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
   int fth = 0, fns = 0, fwl = -1, fwr = 0;
   if (const char* f = getenv("TIC_FORCE_TILE")) sscanf(f, "%d,%d,%d,%d", &fth, &fns, &fwl, &fwr);
   if (!fth) fwl = -1;
-  for (int pass = 0; pass < 2; ++pass) {
-    const int fm = pass == 0 ? form : 0;  // no Winograd variant for this signature: direct
-    if (pass == 1 && (form == 0 || fwl >= 0)) break;
+  for (int pass = 0; pass < 3; ++pass) {
+    const int fm = form_fallback(form, pass);  // no variant of this form for the signature: the next
+    if (fm < 0 || (pass > 0 && fwl >= 0)) break;
     const tic::ConvEntry* best = nullptr;
     long best_wgs = -1, best_work = -1;
     bool best_ok = false;
@@ -196,7 +208,7 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
       if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
       if (fth && (c.th != fth || c.nsplit != fns || (fwr > 0 && c.wr != fwr))) continue;
       if (!form_match(c, fm, fwl)) continue;
-      const int cols = c.wlds == 4 ? 32 * c.wr / (c.th / 2) : 16;  // output columns per workgroup
+      const int cols = c.wlds == 4 ? 32 * c.wr / (c.th / 2) : (c.wlds == 5 ? 256 / c.th : 16);  // output columns / WG
       const long wgs = (long)((wg + cols - 1) / cols) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
       const long work = (long)c.th * cols * 4 / c.nsplit;  // pixels x channel-fraction per workgroup
       const bool ok = wgs >= 512;
@@ -225,11 +237,12 @@ std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, 
   int cnt = 0;
   const tic::ConvEntry* e = regs[mode](&cnt);
   std::vector<const tic::ConvEntry*> out;
-  for (int pass = 0; pass < 2 && out.empty(); ++pass) {
-    const int fm = pass == 0 ? form : 0;
+  for (int pass = 0; pass < 3 && out.empty(); ++pass) {
+    const int fm = form_fallback(form, pass);
+    if (fm < 0) break;
     for (int i = 0; i < cnt; ++i)
       if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
-          e[i].out == outm && (e[i].wlds == 4) == (fm == 1))
+          e[i].out == outm && e[i].wlds != 3 && entry_form(e[i]) == fm)
         out.push_back(&e[i]);
   }
   return out;
@@ -270,6 +283,34 @@ void pack_wino(const float* k, int cin, int cout, std::vector<float>* wp) {
           for (int ky = 0; ky < 3; ++ky)
             for (int kx = 0; kx < 3; ++kx) u += G[xi][ky] * g[ky][kx] * G[nu][kx];
           (*wp)[((((size_t)(xi * 4 + nu) * KC + kc) * 4 + gg) * cout + co) * 4 + t] = (float)u;
+        }
+    }
+}
+
+// Winograd F(4x4,3x3) weights U = G g G^T on the points (0, 1, -1, 2, -1/2, inf) per
+// (ci, co), in double and rounded once, packed [36 p = 6 xi + nu][Cin/16][4 g][Cout][4 t]
+// (conv3x3_wino4.h: A^T G B^T with the B^T / A^T there is exactly the 3-tap correlation).
+void pack_wino4(const float* k, int cin, int cout, std::vector<float>* wp) {
+  static const double G[6][3] = {{1, 0, 0},
+                                 {-1.0 / 3, -1.0 / 3, -1.0 / 3},
+                                 {1.0 / 3, -1.0 / 3, 1.0 / 3},
+                                 {1.0 / 15, 2.0 / 15, 4.0 / 15},
+                                 {-16.0 / 15, 8.0 / 15, -4.0 / 15},
+                                 {0, 0, 1}};
+  const int KC = cin / 16;
+  wp->assign((size_t)36 * cin * cout, 0.f);
+  for (int ci = 0; ci < cin; ++ci)
+    for (int co = 0; co < cout; ++co) {
+      double g[3][3];
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx) g[ky][kx] = k[((size_t)(ky * 3 + kx) * cin + ci) * cout + co];
+      const int kc = ci / 16, gg = (ci % 16) / 4, t = ci % 4;
+      for (int xi = 0; xi < 6; ++xi)
+        for (int nu = 0; nu < 6; ++nu) {
+          double u = 0;
+          for (int ky = 0; ky < 3; ++ky)
+            for (int kx = 0; kx < 3; ++kx) u += G[xi][ky] * g[ky][kx] * G[nu][kx];
+          (*wp)[((((size_t)(xi * 6 + nu) * KC + kc) * 4 + gg) * cout + co) * 4 + t] = (float)u;
         }
     }
 }
@@ -334,6 +375,7 @@ struct LayerRT {
   float* d_w2 = nullptr;  // alternate packing (last layer: scatter form)
   float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
   float* d_ww = nullptr;  // stride-1 layers: Winograd-packed U (conv3x3_wino.h)
+  float* d_ww4 = nullptr; // 64 -> 64 stride-1 layers: F(4x4,3x3) U (conv3x3_wino4.h)
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
@@ -398,7 +440,7 @@ struct tic_handle {
   bool use_graph = false;
   bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); default: struct_defaults
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
-  int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3)
+  int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3), 2 F(4x4,3x3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
@@ -438,10 +480,12 @@ static void touch(tic_handle* h) { h->stream_dirty = true; }
 // Key of a layer's tuned-tiling map: the batch size, per stride-1 form (each form has its
 // own candidate set, so switching the form never reuses the other form's choice).
 static int tkey(const tic_handle* h, const LayerRT& l, int n) {
-  return l.def.kind == K_S1 && h->s1_form == 1 ? n + (1 << 24) : n;
+  return l.def.kind == K_S1 && h->s1_form > 0 ? n + (h->s1_form << 24) : n;
 }
 static int layer_form(const tic_handle* h, const LayerRT& l) { return l.def.kind == K_S1 ? h->s1_form : 0; }
-static const float* conv_weights(const LayerRT& l, const tic::ConvEntry* e) { return e->wlds == 4 ? l.d_ww : l.d_w; }
+static const float* conv_weights(const LayerRT& l, const tic::ConvEntry* e) {
+  return e->wlds == 4 ? l.d_ww : (e->wlds == 5 ? l.d_ww4 : l.d_w);
+}
 
 namespace {
 
@@ -604,14 +648,16 @@ StructDefaults struct_defaults(int model_id) {
   return {true, true, small_stages};
 }
 
-// Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino, else built-in.
-const int kS1FormDefault = 1;
-int default_s1_form() {
+// Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino|wino4, else built-in:
+// F(2x2,3x3) for every model (models 0-2 run their 16x16 stages in the F(2x2,3x3) chain).
+int default_s1_form(int model_id) {
   const char* f = getenv("TIC_S1_FORM");
   const std::string s = f ? f : "";
+  if (s == "wino4") return 2;
   if (s == "wino") return 1;
   if (s == "direct") return 0;
-  return kS1FormDefault;
+  (void)model_id;
+  return 1;
 }
 
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
@@ -1237,7 +1283,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   h->act_elems = act;
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
-  h->s1_form = default_s1_form();
+  h->s1_form = default_s1_form(model_id);
   {
     const StructDefaults sd = struct_defaults(model_id);
     h->fuse01 = sd.fuse01;
@@ -1273,6 +1319,7 @@ void tic_destroy(tic_handle* h) {
     if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
+    if (l.d_ww4) (void)hipFree(l.d_ww4);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
@@ -1374,13 +1421,19 @@ int tic_finalize(tic_handle* h) {
     if (l.d_w2) (void)hipFree(l.d_w2);
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
+    if (l.d_ww4) (void)hipFree(l.d_ww4);
     if (l.d_b) (void)hipFree(l.d_b);
-    l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_b = nullptr;
+    l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_ww4 = l.d_b = nullptr;
     if (l.def.kind == K_S1 && i > 0 && i < L - 1) {
       std::vector<float> ww;
       pack_wino(l.k.data(), l.def.cin, l.def.cout, &ww);
       HIP_TRY(hipMalloc((void**)&l.d_ww, ww.size() * sizeof(float)));
       HIP_TRY(hipMemcpy(l.d_ww, ww.data(), ww.size() * sizeof(float), hipMemcpyHostToDevice));
+      if (l.def.cin == 64 && l.def.cout == 64) {  // the widths conv3x3_wino4.h is compiled for
+        pack_wino4(l.k.data(), l.def.cin, l.def.cout, &ww);
+        HIP_TRY(hipMalloc((void**)&l.d_ww4, ww.size() * sizeof(float)));
+        HIP_TRY(hipMemcpy(l.d_ww4, ww.data(), ww.size() * sizeof(float), hipMemcpyHostToDevice));
+      }
     }
     if (i == L - 2 && l.def.kind == K_T2) {  // raw kernel for the fused decoder tail's halo
       HIP_TRY(hipMalloc((void**)&l.d_w3, l.k.size() * sizeof(float)));
@@ -1624,11 +1677,11 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->chain_order = value != 0;
     return TIC_OK;
   }
-  if (k == "s1_form") {  // 0 direct, 1 Winograd, -1 the default (TIC_S1_FORM or built-in)
-    if (value < -1 || value > 1) return fail(TIC_EINVAL, "s1_form must be -1, 0 or 1");
+  if (k == "s1_form") {  // 0 direct, 1 Winograd F(2,3), 2 F(4,3), -1 the default (TIC_S1_FORM or built-in)
+    if (value < -1 || value > 2) return fail(TIC_EINVAL, "s1_form must be -1, 0, 1 or 2");
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
-    h->s1_form = value < 0 ? default_s1_form() : value;
+    h->s1_form = value < 0 ? default_s1_form(h->model_id) : value;
     return TIC_OK;
   }
   return fail(TIC_EINVAL, "unknown option %s", key);
@@ -2126,7 +2179,10 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
                             : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
                                         last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
-    if (e->wlds == 4)
+    if (e->wlds == 5)
+      snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4, e->act,
+               tf[e->res != 0], e->in, e->out);
+    else if (e->wlds == 4)
       snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
                e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
     else if (e->wlds == 3)
@@ -2193,7 +2249,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       if (sscanf(ln.c_str(), "flag %31s %d", name, &a) != 2) return fail(TIC_EINVAL, "tuning line %d", line);
       if (!strcmp(name, "fuse01")) fuse01 = a != 0;
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
-      else if (!strcmp(name, "s1_form") && (a == 0 || a == 1)) s1_form = a;
+      else if (!strcmp(name, "s1_form") && a >= 0 && a <= 2) s1_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
       else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 4) chain_wh = a;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
@@ -2257,6 +2313,7 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
                 d_res ? 1 : 0);
   std::vector<float> wp;
   if (e->wlds == 4) pack_wino(w_host, cin, cout, &wp);
+  else if (e->wlds == 5) pack_wino4(w_host, cin, cout, &wp);
   else pack_generic(w_host, kind, cin, cout, &wp);
   Scratch s_w, s_b;
   HIP_TRY(s_w.alloc(wp.size() * 4));
