@@ -29,6 +29,13 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 # Winograd F(2x2,3x3): 16 transform points per 2x2 output tile instead of 4 x 9 taps, so
 # the minimal-form FLOP count of a stride-1 layer run in that form is 16/36 of the direct one
 WINO_FRAC = 16.0 / 36.0
+# Winograd F(4x4,3x3) (s1_form 2, conv3x3_wino4_kernel): 36 points per 4x4 tile, 36/144 = 1/4
+WINO4_FRAC = 36.0 / 144.0
+
+
+def wino_frac(kernel):
+    """Minimal-form share of the direct-form FLOPs for a layer run by `kernel`."""
+    return WINO4_FRAC if "wino4" in kernel else (WINO_FRAC if "wino" in kernel else 1.0)
 
 
 def parse():
@@ -117,8 +124,7 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
         launch = []
         for k in kernels:
             launch.append(k if k or not launch else launch[-1])
-        work = [(lay, f * WINO_FRAC if "wino" in launch[i] else f, b, ho)
-                for i, (lay, f, b, ho) in enumerate(work)]
+        work = [(lay, f * wino_frac(launch[i]), b, ho) for i, (lay, f, b, ho) in enumerate(work)]
 
     def out_res_bytes(i):
         lay, _, _, ho = work[i]
@@ -189,12 +195,14 @@ def step_roofline(rows, batch, step_ms):
 
 
 def winograd_note(roof, kernels, flops, ms):
-    """A Winograd F(2x2,3x3) group's FLOPs are already the minimal-form count (16/36 of the
-    direct form: kernel_groups), so `achieved`/`frac` are what the matrix cores ran and
-    frac <= 1; the direct-form equivalent rate is reported beside it."""
+    """A Winograd group's FLOPs are already the minimal-form count (F(2x2,3x3): 16/36,
+    F(4x4,3x3): 36/144 of the direct form: kernel_groups), so `achieved`/`frac` are what the
+    matrix cores ran and frac <= 1; the direct-form equivalent rate is reported beside it."""
     if kernels and all("wino" in k for k in kernels):
-        roof["flop_form"] = "winograd F(2x2,3x3) minimal form: 16/36 of the direct-form FLOPs"
-        roof["direct_equiv_tflops"] = round(flops / WINO_FRAC / (ms * 1e-3) / 1e12, 2)
+        f4 = all("wino4" in k for k in kernels)
+        roof["flop_form"] = ("winograd F(4x4,3x3) minimal form: 36/144 of the direct-form FLOPs" if f4 else
+                             "winograd F(2x2,3x3) minimal form: 16/36 of the direct-form FLOPs")
+        roof["direct_equiv_tflops"] = round(flops / wino_frac(kernels[0]) / (ms * 1e-3) / 1e12, 2)
 
 
 def launch_units(layer_names, kernels, names):

@@ -2180,8 +2180,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
                                         last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
     if (e->wlds == 5)
-      snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4, e->act,
-               tf[e->res != 0], e->in, e->out);
+      snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4,
+               e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
     else if (e->wlds == 4)
       snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
                e->nsplit, e->act, tf[e->res != 0], e->in, e->out);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Winograd F(4x4,3x3) (s1_form 2): parity tests, then model_3 configs[2] tuned in the run in
-# form 2 and in form 1 on the same box (tuned states saved to gpurun_out/).
+# form 2 (tuned state saved to gpurun_out/).
 set -e
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -v --timeout 200 \
@@ -8,6 +8,3 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
 TIC_S1_FORM=wino4 TIC_TUNE_LOG=1 timeout -k 10 500 python -u bench.py --no-cpu-baseline --model 3 --batch 256 \
   --steps 30 --warmup 5 --tune-cache gpurun_out/tune_model3_b256_f2.json \
   --layers-out gpurun_out/bench_layers_m3_f2.json > gpurun_out/bench_m3_f2.json 2> gpurun_out/bench_m3_f2.err
-timeout -k 10 500 python -u bench.py --no-cpu-baseline --model 3 --batch 256 --steps 30 --warmup 5 \
-  --tune-cache gpurun_out/tune_model3_b256_f1.json \
-  --layers-out gpurun_out/bench_layers_m3_f1.json > gpurun_out/bench_m3_f1.json 2> gpurun_out/bench_m3_f1.err
