@@ -13,9 +13,9 @@
 // 6e-6 for the usual (0, +-1, +-2); model_3 end to end: pre-activations 9e-7 relative, no
 // symbol changes, decoder 6e-3 on the [0,255] scale against the 1e-2 bar).
 //
-// Workgroup: 16 4x4 tiles (TTY rows x 16/TTY columns of tiles; TTY = 1, 2, 4 for 64-, 32-,
-// 16-wide layers) x one or both output-channel halves (NSPLIT, below).  The wave owning
-// B^T row xi and an output-channel half forms row xi of B^T d from the staged input rows (rows 1..4
+// Workgroup: 768 threads = 12 waves (3 per SIMD), 16 4x4 tiles (TTY rows x 16/TTY columns of
+// tiles; TTY = 1, 2, 4 for 64-, 32-, 16-wide layers).  Wave w owns B^T row xi = w / 2 and
+// output-channel half w % 2: it forms row xi of B^T d from the staged input rows (rows 1..4
 // always, row 0 / 5 for xi = 0 / 5 — the non-zeros of B^T), then the six column
 // combinations V_(xi,nu) in registers, and runs the six point GEMMs (M = Cout / 2, N = 16
 // tiles, K = Cin) on v_mfma_f32_16x16x4_f32 with conv3x3_kernel's fragment layout.  The
@@ -27,6 +27,13 @@
 // (T = M A), the waves swap T through LDS (aliasing the dead input tile) and each thread
 // finishes Y = A^T T for one (tile, output column, 4-channel quad), then my_conv2d's epilogue.
 //
+// One workgroup per CU (104-117 KB of LDS, 168 VGPRs at 3 waves per SIMD).  Measured and not
+// kept: two 384-thread workgroups per tile splitting the output channels, each staging the
+// input in two channel halves (65 KB, two per CU): 1.4x slower; a persistent tiling walking
+// tiles with the next tile's input in registers (loaded while the output transform and the
+// stores of the current one run): 5-15 % slower (it spills, and the staging wait it hides is
+// a small part — rocprofv3 SQ counters).
+//
 // Summation order per output is fixed by the code — M over K in MFMA order, the transforms
 // in the orders written below — and does not depend on TTY: the tilings of this form are
 // bit-identical to each other.  Different from forms 0 and 1 by rounding only.
@@ -35,7 +42,8 @@
 
 namespace tic {
 
-// B^T (rows xi, columns i) and A^T (rows a, columns nu) of F(4x4, 3x3) on (0, 1, -1, 2, -1/2)
+// B^T (rows xi, columns i) and A^T (rows a, columns nu) of F(4x4, 3x3) on (0, 1, -1, 2, -1/2);
+// w4_bt / w4_at below apply them factored, the row coefficients of B^T are read from the table
 __device__ constexpr float kW4BT[6][6] = {{1.f, 1.5f, -2.f, -1.5f, 1.f, 0.f},  {0.f, -1.f, -2.5f, -0.5f, 1.f, 0.f},
                                           {0.f, 1.f, 0.5f, -2.5f, 1.f, 0.f},   {0.f, -0.5f, -1.f, 0.5f, 1.f, 0.f},
                                           {0.f, 2.f, -1.f, -2.f, 1.f, 0.f},    {0.f, 1.f, 1.5f, -2.f, -1.5f, 1.f}};
@@ -44,28 +52,34 @@ __device__ constexpr float kW4AT[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
                                           {0.f, 1.f, 1.f, 4.f, 0.25f, 0.f},
                                           {0.f, 1.f, -1.f, 8.f, -0.125f, 1.f}};
 
+typedef unsigned int w4u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ f32x4 fma4s(float c, f32x4 x, f32x4 y) {
   return f32x4{__builtin_fmaf(c, x.x, y.x), __builtin_fmaf(c, x.y, y.y), __builtin_fmaf(c, x.z, y.z),
                __builtin_fmaf(c, x.w, y.w)};
 }
 
-// sum_j k[j] v[j] over the non-zero k[j] in index order: the first term k * v, then fmas
-// (k a compile-time row after unrolling: the zero terms vanish, the +-1 products are exact)
-template <int N>
-__device__ __forceinline__ f32x4 wcomb(const float (&k)[N], const f32x4 (&v)[N]) {
-  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-  bool first = true;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    if (k[j] == 0.f) continue;
-    if (first) {
-      s = k[j] * v[j];
-      first = false;
-    } else {
-      s = fma4s(k[j], v[j], s);
-    }
-  }
-  return s;
+// V_nu = sum_j BT[nu][j] r_j for all six nu, factored (16 operations instead of 26):
+// a = r1 - r3, b = r4 - r2, u = r1 + r2 / 2, w = u + r2.
+__device__ __forceinline__ void w4_bt(const f32x4 (&r)[6], f32x4 (&V)[6]) {
+  const f32x4 a = r[1] - r[3], b = r[4] - r[2];
+  V[3] = fma4s(-0.5f, a, b);
+  V[4] = fma4s(2.f, a, b);
+  V[0] = (fma4s(1.5f, a, r[0]) + b) - r[2];
+  const f32x4 u = fma4s(0.5f, r[2], r[1]);
+  V[2] = fma4s(-2.5f, r[3], r[4] + u);
+  V[1] = b - fma4s(0.5f, r[3], u + r[2]);
+  V[5] = (fma4s(-1.5f, b, a) - r[3]) + r[5];
+}
+
+// T_b = sum_nu AT[b][nu] M_nu for the four b, factored (12 operations instead of 18):
+// s = M1 + M2, d = M1 - M2.
+__device__ __forceinline__ void w4_at(const f32x4 (&M)[6], f32x4 (&T)[4]) {
+  const f32x4 s = M[1] + M[2], d = M[1] - M[2];
+  T[0] = ((M[0] + s) + M[3]) + M[4];
+  T[1] = fma4s(-0.5f, M[4], fma4s(2.f, M[3], d));
+  T[2] = fma4s(0.25f, M[4], fma4s(4.f, M[3], s));
+  T[3] = fma4s(-0.125f, M[4], fma4s(8.f, M[3], d)) + M[5];
 }
 
 template <int TTY>
@@ -79,116 +93,96 @@ struct Wino4Geom {
 };
 
 // Weights (ConvArgs::wp): U packed [36 p][Cin/16][4 g][Cout][4 t], p = 6 xi + nu.
-// NSPLIT 1: 768 threads, wave w = (xi = w / 2, output-channel half w % 2), the whole Cin of
-// the input tile staged at once (117 KB: one workgroup per CU).  NSPLIT 2: two 384-thread
-// workgroups per tile, one per output-channel half (wave = xi), each staging the input tile
-// in two channel halves (65 KB: two workgroups per CU, so one's staging and stores overlap
-// the other's matrix work).  Same per-output operation order: bit-identical.
-template <int CIN, int COUT, int TTY, int NSPLIT, int ACT, bool RES, int IN, int OUT>
-__global__ void __launch_bounds__(NSPLIT == 1 ? 768 : 384, 3) conv3x3_wino4_kernel(const ConvArgs a) {
+template <int CIN, int COUT, int TTY, int ACT, bool RES, int IN, int OUT>
+__global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   using G = Wino4Geom<TTY>;
   constexpr int NT = G::NT, TTX = G::TTX, LR = G::LR, LCOL = G::LCOL, HPP = G::HPP;
-  static_assert(CIN % 32 == 0 && COUT % 32 == 0 && (NSPLIT == 1 || NSPLIT == 2), "channels");
-  constexpr int NTHR = NSPLIT == 1 ? 768 : 384;
-  constexpr int KST = CIN / NSPLIT;            // input channels staged at once
-  constexpr int NHALF = CIN / KST;             // staging rounds
-  constexpr int PS = KST + 8, KC = CIN / 16, KCH = KST / 16, C4 = KST / 4;
+  static_assert(CIN % 16 == 0 && COUT % 32 == 0, "channels");
+  static_assert(IN == IN_F32 && OUT == OUT_F32, "f32 input and output only (the res-block convs)");
+  constexpr int NTHR = 768;
+  constexpr int PS = CIN + 8, KC = CIN / 16, C4 = CIN / 4;
   constexpr int RS = 4 * HPP * PS + G::RPAD;  // floats per staged row
   constexpr int TILE = LR * RS;
   constexpr int CW = COUT / 2;                // output channels per wave
   constexpr int NBW = CW / 16;
-  constexpr int CWG = COUT / NSPLIT;          // output channels per workgroup
-  constexpr int XS = CWG + 4;                 // exchange pitch per (xi, b, tile)
+  constexpr int XS = COUT + 4;                // exchange pitch per (xi, b, tile)
   constexpr int XCH = 24 * NT * XS;           // [6 xi][4 b][NT][XS]
   __shared__ __attribute__((aligned(16))) float smem[TILE > XCH ? TILE : XCH];
 
   const int tid = threadIdx.x;
-  int bx, by, bz;
-  xcd_tile(bx, by, bz);
-  const int split = NSPLIT > 1 ? bx % NSPLIT : 0;
-  if (NSPLIT > 1) bx /= NSPLIT;
-  const int oy0 = by * 4 * TTY, ox0 = bx * 4 * TTX, nimg = bz;
-  const int H = a.H, W = a.W;
+  const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int xi = NSPLIT == 1 ? wave >> 1 : wave;
-  const int co_w = (NSPLIT == 1 ? (wave & 1) : split) * CW;  // first output channel of this wave
-  const int co_x = NSPLIT == 1 ? co_w : 0;                    // ... within the exchange
+  const int xi = wave >> 1, co_w = (wave & 1) * CW;
   const int lane = tid & 63, li = lane & 15, lg = lane >> 4;
 
-  // ---- A fragments (U) from L2, prefetched PF steps ahead; step s = 6 kc + nu ----
-  constexpr int NSTEP = 6 * KC, PF = NSPLIT == 1 ? 2 : 1;
-  const float* __restrict__ wl = a.wp + (size_t)6 * xi * KC * 16 * COUT + (size_t)(lg * COUT + co_w + li) * 4;
-  auto wglob = [&](int s, int nb) -> f32x4 {
-    const int kc = s / 6, nu = s % 6;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * COUT + nb * 64);
-  };
-  f32x4 av[PF + 1][NBW];
-#pragma unroll
-  for (int p = 0; p < PF; ++p)
-#pragma unroll
-    for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(p, nb);
+  int bx, by, bz;
+  xcd_tile(bx, by, bz);
+  const int oy0 = by * 4 * TTY, ox0 = bx * 4 * TTX, nimg = bz;
 
-  // ---- stage channels [KST h, KST (h+1)) of the input tile, columns split by (column mod 4);
-  // zero outside the image ----
+  // ---- stage the input tile (all Cin, columns split by (column mod 4), zero outside the
+  // image): global loads into registers, then LDS writes ----
   constexpr int NSTAGE = LR * LCOL * C4;
   constexpr int NIT = (NSTAGE + NTHR - 1) / NTHR;
-  constexpr int SBM = NSPLIT == 1 ? 10 : 5;  // loads in flight per thread (the second half's
-                                            // staging runs beside live accumulators)
-  constexpr int SB = NIT < SBM ? NIT : SBM;
-  auto stage = [&](int h) {
+  f32x4 pre[NIT];
+  // element i of this thread: channel quad c4 = tid % C4 (C4 divides NTHR), pixel
+  // tid / C4 + i NTHR / C4 of the tile, walked incrementally (row, col) — no divisions
+  static_assert(NTHR % C4 == 0, "channel quad per thread");
+  constexpr int DP = NTHR / C4, DR = DP / LCOL, DC = DP % LCOL;
+  auto walk = [&](auto&& fn) {
+    int t = tid;  // opaque copy: the index math is re-derived at each use instead of held live
+    asm volatile("" : "+v"(t));
+    const int c4 = t % C4, p0 = t / C4;
+    int row = p0 / LCOL, col = p0 - (p0 / LCOL) * LCOL;
 #pragma unroll
-    for (int i0 = 0; i0 < NIT; i0 += SB) {
-      f32x4 tmp[SB];
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        const int e = (i0 + i) * NTHR + tid;
-        tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (i0 + i < NIT && e < NSTAGE) {
-          const int c4 = e % C4, pe = e / C4, col = pe % LCOL, row = pe / LCOL;
-          const int iy = oy0 - 1 + row, ix = ox0 - 1 + col;
-          if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-            const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + h * KST + c4 * 4;
-            if constexpr (IN == IN_F32) {
-              tmp[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
-            } else {
-              const uint32_t q = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(a.in) + off);
-              tmp[i].x = a.lut[q & 0xff];
-              tmp[i].y = a.lut[(q >> 8) & 0xff];
-              tmp[i].z = a.lut[(q >> 16) & 0xff];
-              tmp[i].w = a.lut[q >> 24];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < SB; ++i) {
-        const int e = (i0 + i) * NTHR + tid;
-        if (i0 + i < NIT && e < NSTAGE) {
-          const int c4 = e % C4, pe = e / C4, col = pe % LCOL, row = pe / LCOL;
-          *reinterpret_cast<f32x4*>(&smem[row * RS + ((col & 3) * HPP + (col >> 2)) * PS + c4 * 4]) = tmp[i];
-        }
+    for (int i = 0; i < NIT; ++i) {
+      fn(i, row, col, c4);
+      col += DC;
+      row += DR;
+      if (col >= LCOL) {
+        col -= LCOL;
+        ++row;
       }
     }
+  };
+  // branch-free: a raw buffer load past num_records returns zeros (the SAME padding and the
+  // elements past the tile), so the loads need no control flow around them
+  auto issue = [&]() {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.in), (short)0, 0x7fffffff, 0x00020000);
+    const int base = nimg * H * W * CIN;  // float offset of the patch (< 2^31: the workspace chunk)
+    walk([&](int i, int row, int col, int c4) {
+      const int iy = oy0 - 1 + row, ix = ox0 - 1 + col;
+      const bool in = row < LR && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int off = in ? (base + (iy * W + ix) * CIN + c4 * 4) * 4 : 0x7fffffff;
+      const w4u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      pre[i] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+    });
+  };
+  auto commit = [&]() {
+    walk([&](int i, int row, int col, int c4) {
+      if ((NSTAGE % NTHR == 0 || i + 1 < NIT) || row < LR)
+        *reinterpret_cast<f32x4*>(&smem[row * RS + ((col & 3) * HPP + (col >> 2)) * PS + c4 * 4]) = pre[i];
+    });
   };
 
   // ---- row xi of B^T d for tile li: r_j = sum_i BT[xi][i] d[i][j] over the non-zero i ----
   const int ty = li / TTX, tx = li % TTX;
   const int tbase = (4 * ty) * RS + tx * PS + lg * 4;
-  // the fifth non-zero of row xi: BT[0][0] = BT[5][5] = 1; rows 1-4 add 0 x row 0 (branch-free)
+  // the fifth non-zero of row xi: BT[0][0] = BT[5][5] = 1
   const int re = xi == 5 ? 5 : 0;
   const float c1 = kW4BT[xi][1], c2 = kW4BT[xi][2], c3 = kW4BT[xi][3], c4 = kW4BT[xi][4];
+  // rows 1-4 add 0 x row 0: branch-free (a wave-uniform branch here makes hipcc spill)
   const float ce = (xi == 0 || xi == 5) ? 1.f : 0.f;
-  auto ld = [&](int i, int j, int kcl) -> f32x4 {
-    return *reinterpret_cast<const f32x4*>(&smem[tbase + i * RS + ((j & 3) * HPP + (j >> 2)) * PS + kcl * 16]);
+  auto ld = [&](int i, int j, int kc) -> f32x4 {
+    return *reinterpret_cast<const f32x4*>(&smem[tbase + i * RS + ((j & 3) * HPP + (j >> 2)) * PS + kc * 16]);
   };
-  f32x4 V[6];
   // column j of that row for chunk kc, in the operation order c1 d1 + c2 d2 + c3 d3 + c4 d4 + ce de
-  auto ldcol = [&](int j, int kcl, f32x4 (&d)[5]) {
-    d[0] = ld(1, j, kcl);
-    d[1] = ld(2, j, kcl);
-    d[2] = ld(3, j, kcl);
-    d[3] = ld(4, j, kcl);
-    d[4] = ld(re, j, kcl);
+  auto ldcol = [&](int j, int kc, f32x4 (&d)[5]) {
+    d[0] = ld(1, j, kc);
+    d[1] = ld(2, j, kc);
+    d[2] = ld(3, j, kc);
+    d[3] = ld(4, j, kc);
+    d[4] = ld(re, j, kc);
   };
   auto rcol = [&](const f32x4 (&d)[5]) {
     f32x4 s = c1 * d[0];
@@ -198,21 +192,33 @@ __global__ void __launch_bounds__(NSPLIT == 1 ? 768 : 384, 3) conv3x3_wino4_kern
     return fma4s(ce, d[4], s);
   };
 
-  f32x4 acc[6][NBW];
-#pragma unroll
-  for (int nu = 0; nu < 6; ++nu)
-#pragma unroll
-    for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ---- A fragments (U) from L2, prefetched PF steps ahead; step s = 6 kc + nu ----
+  constexpr int NSTEP = 6 * KC, PF = 2;
+  const float* wl = a.wp + (size_t)6 * xi * KC * 16 * COUT + (size_t)(lg * COUT + co_w + li) * 4;
+  // (made opaque after the staging below: otherwise hipcc computes every step's 64-bit weight
+  // address up front and spills them)
+  auto wglob = [&](int s, int nb) -> f32x4 {
+    const int kc = s / 6, nu = s % 6;
+    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * COUT + nb * 64);
+  };
+  // the output quad of this thread is the same in every pass of the Y phase (768 % Q4 == 0)
+  constexpr int Q4 = COUT / 4, NTASK = 4 * NT * Q4;
+  static_assert(NTHR % Q4 == 0, "quad per thread");
+  const int q = tid % Q4;
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + 4 * q);
 
-  // Software pipeline: while the MFMAs of point nu of chunk kc issue, column nu of chunk
-  // kc + 1 is read (before them) and combined (after them); the six V of chunk kc + 1 follow
-  // the chunk.  The transform's VALU work thus runs in the matrix pipe's shadow of the same
-  // wave instead of between its MFMA phases.
-#pragma unroll
-  for (int h = 0; h < NHALF; ++h) {
-    if (h > 0) __syncthreads();  // every wave is done with the previous channel half
-    stage(h);
+  issue();
+  {
+    commit();
     __syncthreads();
+    asm volatile("" : "+v"(wl));
+
+    f32x4 av[PF + 1][NBW];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(p, nb);
+    f32x4 V[6];
     {
       f32x4 r[6], d[5];
 #pragma unroll
@@ -220,13 +226,20 @@ __global__ void __launch_bounds__(NSPLIT == 1 ? 768 : 384, 3) conv3x3_wino4_kern
         ldcol(j, 0, d);
         r[j] = rcol(d);
       }
-#pragma unroll
-      for (int nu = 0; nu < 6; ++nu) V[nu] = wcomb(kW4BT[nu], r);
+      w4_bt(r, V);
     }
+    f32x4 acc[6][NBW];
 #pragma unroll
-    for (int kcl = 0; kcl < KCH; ++kcl) {
-      const int kc = h * KCH + kcl;
-      const bool next = kcl + 1 < KCH;
+    for (int nu = 0; nu < 6; ++nu)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Software pipeline: while the MFMAs of point nu of chunk kc issue, column nu of chunk
+    // kc + 1 is read (before them) and combined (after them); the six V of chunk kc + 1
+    // follow the chunk.
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const bool next = kc + 1 < KC;
       f32x4 rn[6], dn[5];
 #pragma unroll
       for (int nu = 0; nu < 6; ++nu) {
@@ -235,70 +248,99 @@ __global__ void __launch_bounds__(NSPLIT == 1 ? 768 : 384, 3) conv3x3_wino4_kern
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
         }
-        if (next) ldcol(nu, kcl + 1, dn);
+        if (next) ldcol(nu, kc + 1, dn);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
-          for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = mfma4(av[s % (PF + 1)][nb][t], V[nu][t], acc[nu][nb]);
+          for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = mfma4(av[s % (PF + 1)][nb][tt], V[nu][tt], acc[nu][nb]);
         __builtin_amdgcn_sched_barrier(0);
         if (next) rn[nu] = rcol(dn);
       }
-      if (next) {
+      if (next) w4_bt(rn, V);
+    }
+
+    // ---- T = M A over nu (per wave), exchanged through LDS (the input tile is dead) ----
+    __syncthreads();
 #pragma unroll
-        for (int nu = 0; nu < 6; ++nu) V[nu] = wcomb(kW4BT[nu], rn);
+    for (int nb = 0; nb < NBW; ++nb) {
+      const f32x4 m[6] = {acc[0][nb], acc[1][nb], acc[2][nb], acc[3][nb], acc[4][nb], acc[5][nb]};
+      f32x4 tb[4];
+      w4_at(m, tb);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        *reinterpret_cast<f32x4*>(&smem[((xi * 4 + b) * NT + li) * XS + co_w + nb * 16 + lg * 4]) = tb[b];
+    }
+
+    // ---- Y = A^T T: one (output column b, tile, 4-channel quad) per thread and pass; the
+    // residuals are read before the exchange barrier so their latency overlaps it ----
+    constexpr int NPASS = (NTASK + NTHR - 1) / NTHR;
+    // per pass: element offset of the task's top output pixel (32-bit: a launch's activation
+    // chunk is < 2^31 floats) and how many of its 4 rows lie inside the image
+    int o0[NPASS], nrow[NPASS];
+    f32x4 rr[NPASS][4];
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const int it = ps * NTHR + tid;
+      const int tile = (it / Q4) % NT, b = it / (Q4 * NT);
+      const int ox = ox0 + 4 * (tile % TTX) + b, oy = oy0 + 4 * (tile / TTX);
+      nrow[ps] = (it < NTASK && ox < Wo) ? min(4, Ho - oy) : 0;
+      o0[ps] = ((nimg * Ho + oy) * Wo + ox) * COUT + 4 * q;
+      if constexpr (RES) {
+#pragma unroll
+        for (int ay = 0; ay < 4; ++ay)
+          rr[ps][ay] = ay < nrow[ps] ? *reinterpret_cast<const f32x4*>(a.res + o0[ps] + ay * Wo * COUT) : f32x4{};
       }
     }
-  }
-
-  // ---- T = M A over nu (per wave), exchanged through LDS (the input tile is dead) ----
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int nb = 0; nb < NBW; ++nb) {
-    const f32x4 m[6] = {acc[0][nb], acc[1][nb], acc[2][nb], acc[3][nb], acc[4][nb], acc[5][nb]};
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const int it = ps * NTHR + tid;
+      if (NTASK % NTHR != 0 && it >= NTASK) break;
+      const int tile = (it / Q4) % NT, b = it / (Q4 * NT);
+      f32x4 T[6];
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
-      *reinterpret_cast<f32x4*>(&smem[((xi * 4 + b) * NT + li) * XS + co_x + nb * 16 + lg * 4]) = wcomb(kW4AT[b], m);
-  }
-  __syncthreads();
-
-  // ---- Y = A^T T: one (output column b, tile, 4-channel quad) per thread and pass ----
-  constexpr int Q4 = CWG / 4, NTASK = 4 * NT * Q4;
-  const int Ho = a.Ho, Wo = a.Wo;
+      for (int x2 = 0; x2 < 6; ++x2)
+        T[x2] = *reinterpret_cast<const f32x4*>(&smem[((x2 * 4 + b) * NT + tile) * XS + 4 * q]);
+      f32x4 Y[4];
+      w4_at(T, Y);
 #pragma unroll
-  for (int it0 = 0; it0 < NTASK; it0 += NTHR) {
-    const int it = it0 + tid;
-    if (NTASK % NTHR != 0 && it >= NTASK) break;
-    const int q = it % Q4, tile = (it / Q4) % NT, b = it / (Q4 * NT);
-    const int tty = tile / TTX, ttx = tile % TTX;
-    const int ox = ox0 + 4 * ttx + b;
-    f32x4 T[6];
-#pragma unroll
-    for (int x2 = 0; x2 < 6; ++x2) T[x2] = *reinterpret_cast<const f32x4*>(&smem[((x2 * 4 + b) * NT + tile) * XS + 4 * q]);
-    if (ox >= Wo) continue;
-    const int co = split * CWG + 4 * q;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + co);
-#pragma unroll
-    for (int ay = 0; ay < 4; ++ay) {
-      const int oy = oy0 + 4 * tty + ay;
-      if (oy >= Ho) break;
-      conv_out4<ACT, RES, OUT>(a, wcomb(kW4AT[ay], T), bb, ((size_t)(nimg * Ho + oy) * Wo + ox) * COUT + co);
+      for (int ay = 0; ay < 4; ++ay) {
+        if (ay >= nrow[ps]) continue;
+        // my_conv2d's epilogue (conv_out4's operations and order): + bias, ReLU, + residual
+        f32x4 v = Y[ay];
+        v.x = __fadd_rn(v.x, bb.x);
+        v.y = __fadd_rn(v.y, bb.y);
+        v.z = __fadd_rn(v.z, bb.z);
+        v.w = __fadd_rn(v.w, bb.w);
+        if constexpr (ACT == ACT_RELU) {
+          v.x = fmaxf(v.x, 0.f);
+          v.y = fmaxf(v.y, 0.f);
+          v.z = fmaxf(v.z, 0.f);
+          v.w = fmaxf(v.w, 0.f);
+        }
+        if constexpr (RES) {
+          v.x = __fadd_rn(v.x, rr[ps][ay].x);
+          v.y = __fadd_rn(v.y, rr[ps][ay].y);
+          v.z = __fadd_rn(v.z, rr[ps][ay].z);
+          v.w = __fadd_rn(v.w, rr[ps][ay].w);
+        }
+        *reinterpret_cast<f32x4*>(a.out + o0[ps] + ay * Wo * COUT) = v;
+      }
     }
   }
 }
 
-template <int CIN, int COUT, int TTY, int NSPLIT, int ACT, bool RES, int IN, int OUT>
+template <int CIN, int COUT, int TTY, int ACT, bool RES, int IN, int OUT>
 static void launch_wino4(const ConvArgs& a, int n, hipStream_t s) {
   constexpr int OW = 4 * Wino4Geom<TTY>::TTX, OH = 4 * TTY;
-  dim3 grid(((a.Wo + OW - 1) / OW) * NSPLIT, (a.Ho + OH - 1) / OH, n);
-  hipLaunchKernelGGL((conv3x3_wino4_kernel<CIN, COUT, TTY, NSPLIT, ACT, RES, IN, OUT>), grid,
-                     dim3(NSPLIT == 1 ? 768 : 384), 0, s, a);
+  dim3 grid((a.Wo + OW - 1) / OW, (a.Ho + OH - 1) / OH, n);
+  hipLaunchKernelGGL((conv3x3_wino4_kernel<CIN, COUT, TTY, ACT, RES, IN, OUT>), grid, dim3(768), 0, s, a);
 }
 
 }  // namespace tic
 
 // Winograd F(4x4,3x3) entry: th = output rows per workgroup (4 TTY), 256 / th columns,
 // weight source 5 = the F(4x4,3x3) packing of U (passed as ConvArgs::wp).
-#define TIC_WINO4(CIN, COUT, TTY, NSPLIT, ACT, RES, IN, OUT)                          \
-  { MODE_S1, CIN, COUT, ACT, RES, IN, OUT, 4 * TTY, 1, NSPLIT, 5,                      \
-    &tic::launch_wino4<CIN, COUT, TTY, NSPLIT, ACT, RES, IN, OUT> }
+#define TIC_WINO4(CIN, COUT, TTY, ACT, RES, IN, OUT) \
+  { MODE_S1, CIN, COUT, ACT, RES, IN, OUT, 4 * TTY, 1, 1, 5, &tic::launch_wino4<CIN, COUT, TTY, ACT, RES, IN, OUT> }

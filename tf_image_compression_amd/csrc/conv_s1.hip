@@ -39,14 +39,11 @@
       TIC_WINO(CIN, COUT, 1, 1, 4, ACT, RES, IN, OUT)
 
 // Winograd F(4x4,3x3) tilings (TTY = 1, 2, 4 tile rows: 4x64, 8x32, 16x16 output pixels per
-// workgroup; NSPLIT 1: one 768-thread workgroup per tile, 2: two 384-thread ones) for the 64 -> 64 res-block convs of model_3 and the rmbe net (form 2)
+// workgroup) for the 64 -> 64 res-block convs of model_3 and the rmbe net (form 2)
 #define S1_WINO4(ACT, RES, IN, OUT)                 \
-  TIC_WINO4(64, 64, 1, 1, ACT, RES, IN, OUT),       \
-      TIC_WINO4(64, 64, 2, 1, ACT, RES, IN, OUT),   \
-      TIC_WINO4(64, 64, 4, 1, ACT, RES, IN, OUT),   \
-      TIC_WINO4(64, 64, 1, 2, ACT, RES, IN, OUT),   \
-      TIC_WINO4(64, 64, 2, 2, ACT, RES, IN, OUT),   \
-      TIC_WINO4(64, 64, 4, 2, ACT, RES, IN, OUT)
+  TIC_WINO4(64, 64, 1, ACT, RES, IN, OUT),          \
+      TIC_WINO4(64, 64, 2, ACT, RES, IN, OUT),      \
+      TIC_WINO4(64, 64, 4, ACT, RES, IN, OUT)
 
 namespace tic {
 // new entries go at the end: tuning files name entries by their index in this table

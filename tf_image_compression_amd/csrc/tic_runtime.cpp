@@ -649,15 +649,16 @@ StructDefaults struct_defaults(int model_id) {
 }
 
 // Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino|wino4, else built-in:
-// F(2x2,3x3) for every model (models 0-2 run their 16x16 stages in the F(2x2,3x3) chain).
+// F(4x4,3x3) for model_3's 64x64 / 32x32 residual stages and the rmbe net (measured: model_3
+// configs[2] 2.84 -> 3.45 GPix/s), F(2x2,3x3) for models 0-2, whose 16x16
+// stages run in the F(2x2,3x3) chain (an 8x8 region holds only four 4x4 tiles).
 int default_s1_form(int model_id) {
   const char* f = getenv("TIC_S1_FORM");
   const std::string s = f ? f : "";
   if (s == "wino4") return 2;
   if (s == "wino") return 1;
   if (s == "direct") return 0;
-  (void)model_id;
-  return 1;
+  return model_id == 3 || model_id == TIC_MODEL_RMBE ? 2 : 1;
 }
 
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
@@ -2180,8 +2181,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
                                         last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
     if (e->wlds == 5)
-      snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4,
-               e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
+      snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4, e->act,
+               tf[e->res != 0], e->in, e->out);
     else if (e->wlds == 4)
       snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
                e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
