@@ -77,10 +77,13 @@ def test_wino_chain_oversubscribed_grid():
 
 
 def test_wino_chain_rmbe_bit_identical():
+    """The chain on the rmbe net's 32x32 stage, in the F(2x2,3x3) form it computes (the net's
+    default stride-1 form is F(4x4,3x3), which the chain does not run)."""
     from tf_image_compression_amd.topology import RMBE_ID
     r = np.random.default_rng(8)
     win = np.clip(r.normal(120, 50, (5, 128, 128, 3)), 0, 255).astype(np.float32)
     with _codec(RMBE_ID, 128) as c:
+        c.set_option("s1_form", 1)
         c.set_option("chain", 0)
         a = c.rmbe_windows(win)
         c.set_option("chain", 1)
