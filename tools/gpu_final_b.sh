@@ -8,6 +8,7 @@ cd $R
 source tools/gpu_steps.sh
 O=$R/gpurun_out
 T=$R/tf_image_compression_amd/tune
+step gputest_chain_$TAG 300 python -u -m pytest tests/test_gpu_chain.py -v --timeout 120 --timeout-method thread
 step pmc_m0_$TAG 400 bash tools/pmc_box.sh m0_$TAG $T/model0_p256_b64_s2.json
 cp $O/pmc_m0_$TAG/traffic.json tools/pmc/traffic_model0_lb32.json
 step pmc_m3_$TAG 600 bash tools/pmc_box.sh m3_$TAG $T/model3_p256_b256_s2.json --model 3 --batch 256
@@ -20,3 +21,4 @@ step bench_img_$TAG 400 python bench.py --workload image4k --steps 10 --warmup 2
 step bench_shard_$TAG 400 python bench.py --workload sharded --steps 5 --warmup 1
 cd /tmp && export TMPDIR=/tmp
 step prof_m0_$TAG 300 rocprofv3 --kernel-trace --stats -d $O/prof_m0_$TAG -o p -- python3 $R/bench.py --no-cpu-baseline
+step prof_m3_$TAG 300 rocprofv3 --kernel-trace --stats -d $O/prof_m3_$TAG -o p -- python3 $R/bench.py --no-cpu-baseline --model 3 --batch 256 --steps 50 --warmup 5
