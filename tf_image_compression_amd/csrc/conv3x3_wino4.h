@@ -38,6 +38,8 @@
 // in the orders written below — and does not depend on TTY: the tilings of this form are
 // bit-identical to each other.  Different from forms 0 and 1 by rounding only.
 #pragma once
+#include <algorithm>
+
 #include "conv3x3_wino.h"
 
 namespace tic {
@@ -334,8 +336,19 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
 template <int CIN, int COUT, int TTY, int ACT, bool RES, int IN, int OUT>
 static void launch_wino4(const ConvArgs& a, int n, hipStream_t s) {
   constexpr int OW = 4 * Wino4Geom<TTY>::TTX, OH = 4 * TTY;
-  dim3 grid((a.Wo + OW - 1) / OW, (a.Ho + OH - 1) / OH, n);
-  hipLaunchKernelGGL((conv3x3_wino4_kernel<CIN, COUT, TTY, ACT, RES, IN, OUT>), grid, dim3(768), 0, s, a);
+  // the kernel's element offsets are 32-bit: launch at most 2^31 input / output floats at a
+  // time (the codec's chunks are far below that; the per-layer entry takes any batch)
+  const size_t per = (size_t)a.H * a.W * CIN > (size_t)a.Ho * a.Wo * COUT ? (size_t)a.H * a.W * CIN
+                                                                           : (size_t)a.Ho * a.Wo * COUT;
+  const int step = (int)std::min<size_t>((size_t)n, ((size_t)1 << 31) / per - 1);
+  for (int n0 = 0; n0 < n; n0 += step) {
+    ConvArgs b = a;
+    b.in = reinterpret_cast<const float*>(a.in) + (size_t)n0 * a.H * a.W * CIN;
+    b.out = a.out + (size_t)n0 * a.Ho * a.Wo * COUT;
+    if (a.res) b.res = a.res + (size_t)n0 * a.Ho * a.Wo * COUT;
+    dim3 grid((a.Wo + OW - 1) / OW, (a.Ho + OH - 1) / OH, std::min(step, n - n0));
+    hipLaunchKernelGGL((conv3x3_wino4_kernel<CIN, COUT, TTY, ACT, RES, IN, OUT>), grid, dim3(768), 0, s, b);
+  }
 }
 
 }  // namespace tic

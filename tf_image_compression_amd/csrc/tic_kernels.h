@@ -27,7 +27,6 @@ struct ConvArgs {
   float qscale;        // Q - 1
   int num_cus;         // compute units (persistent variants size their grid from it)
   int grid_cap;        // > 0: cap on the persistent grid (tests force several tiles per workgroup)
-  int batch;           // patches (set by the launcher; persistent grids derive their tile count from it)
 };
 
 struct RgbInArgs {
