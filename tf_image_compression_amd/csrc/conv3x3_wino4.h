@@ -336,11 +336,12 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
 template <int CIN, int COUT, int TTY, int ACT, bool RES, int IN, int OUT>
 static void launch_wino4(const ConvArgs& a, int n, hipStream_t s) {
   constexpr int OW = 4 * Wino4Geom<TTY>::TTX, OH = 4 * TTY;
-  // the kernel's element offsets are 32-bit: launch at most 2^31 input / output floats at a
-  // time (the codec's chunks are far below that; the per-layer entry takes any batch)
+  // the kernel's offsets are 32-bit (input: buffer byte offsets below 2^31, so < 2^29 floats;
+  // output: element offsets): launch at most 2^29 floats of either at a time (the codec's
+  // chunks are far below that; the per-layer entry takes any batch)
   const size_t per = (size_t)a.H * a.W * CIN > (size_t)a.Ho * a.Wo * COUT ? (size_t)a.H * a.W * CIN
                                                                            : (size_t)a.Ho * a.Wo * COUT;
-  const int step = (int)std::min<size_t>((size_t)n, ((size_t)1 << 31) / per - 1);
+  const int step = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, (((size_t)1 << 29) - 1) / per));
   for (int n0 = 0; n0 < n; n0 += step) {
     ConvArgs b = a;
     b.in = reinterpret_cast<const float*>(a.in) + (size_t)n0 * a.H * a.W * CIN;

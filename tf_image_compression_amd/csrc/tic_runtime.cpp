@@ -208,6 +208,9 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
       if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
       if (fth && (c.th != fth || c.nsplit != fns || (fwr > 0 && c.wr != fwr))) continue;
       if (!form_match(c, fm, fwl)) continue;
+      // F(4x4,3x3) stages a patch through 32-bit buffer byte offsets: patches of >= 2^29
+      // floats run the next form (the codec's 256x256 patches are far below)
+      if (c.wlds == 5 && (long)hg * wg * c.cin >= (1L << 29)) continue;
       const int cols = c.wlds == 4 ? 32 * c.wr / (c.th / 2) : (c.wlds == 5 ? 256 / c.th : 16);  // output columns / WG
       const long wgs = (long)((wg + cols - 1) / cols) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
       const long work = (long)c.th * cols * 4 / c.nsplit;  // pixels x channel-fraction per workgroup
