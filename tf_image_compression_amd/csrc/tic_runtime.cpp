@@ -2043,7 +2043,9 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       }
       if (first || last) {
         const RgbOutForm fm = first ? RgbOutForm{0, tic::rgb_in_variants()} : rgb_out_form();
-        const int keep = first ? l.tuned_var[sizes[0]] : rgb_out_variant(l.tuned_var, sizes[0]);
+        auto iv = l.tuned_var.find(sizes[0]);
+        const int keep = first ? (iv != l.tuned_var.end() ? iv->second : kRgbInDefault)
+                               : rgb_out_variant(l.tuned_var, sizes[0]);
         int best_v = keep;
         float best = cur;
         for (int v = fm.lo; v < fm.hi && !rc; ++v) {
@@ -2063,7 +2065,10 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
         const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
                                      last_enc ? tic::OUT_QUANT : tic::OUT_F32, layer_form(h, l));
-        const tic::ConvEntry* keep = l.tuned[tkey(h, l, sizes[0])];
+        // an untuned size runs find_conv's pick: `keep` is then null and, when no candidate beats
+        // the current step, the size stays untuned (not a null entry, which would drop the layer)
+        auto kt = l.tuned.find(tkey(h, l, sizes[0]));
+        const tic::ConvEntry* keep = kt != l.tuned.end() ? kt->second : nullptr;
         const tic::ConvEntry* best_e = keep;
         float best = cur;
         for (const tic::ConvEntry* c : cands) {
@@ -2079,7 +2084,10 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
             best_e = c;
           }
         }
-        for (int m : sizes) l.tuned[tkey(h, l, m)] = best_e;
+        for (int m : sizes) {
+          if (best_e) l.tuned[tkey(h, l, m)] = best_e;
+          else l.tuned.erase(tkey(h, l, m));
+        }
         cur = best;
       }
     }
