@@ -401,6 +401,7 @@ def main():
     wall0 = time.time()
     for _ in range(args.steps):
         codec.codec_device(d_in, B, d_idx, d_rgb)
+    t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (a host-bound loop shows here)
     codec.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
@@ -448,6 +449,7 @@ def main():
                         images=B * args.steps, t_start=wall0, t_end=wall1)
     gathered = comm.allgather_stats(st)
     summary = dist.combine(gathered)
+    ranks = rank_devices(comm, codec, rank, local)
 
     # the dominant group's roofline from its one-lane (exclusive) launch duration: a
     # kernel-quality figure; beside it the same launches timed in the steady two-lane steps
@@ -520,6 +522,8 @@ def main():
         "roofline_groups": roof_groups,
         "roofline_step_frac": round(step_roofline(rows, B, step_ms), 4),
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "hip_graph": bool(args.graph)},
+        "host_enqueue_ms_per_step": round(t_enq * 1e3 / args.steps, 4),
+        "ranks": ranks,
         "tuning": tuning,
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
                             "raw_bpp": round(summary["bpp"], 4)},
@@ -544,6 +548,19 @@ def main():
         print(json.dumps(out), flush=True)
     comm.close()
     codec.close()
+
+
+def rank_devices(comm, codec, rank, local):
+    """Every rank's (rank, LOCAL_RANK, HIP device, PCI address) through one all-gather: a
+    multi-GPU record shows which devices RCCL joined."""
+    import re
+    info = codec.device_info()
+    m = re.search(r"device (\d+) \| pci ([0-9a-f]+):([0-9a-f]+):([0-9a-f]+)", info)
+    dev, dom, bus, fn = (int(m.group(1)), int(m.group(2), 16), int(m.group(3), 16), int(m.group(4), 16)) if m \
+        else (-1, 0, 0, 0)
+    rows = comm.allgather_f64([rank, local, dev, dom, bus, fn])
+    return [{"rank": int(r[0]), "local_rank": int(r[1]), "device": int(r[2]),
+             "pci": f"{int(r[3]):04x}:{int(r[4]):02x}:{int(r[5]):02x}"} for r in rows]
 
 
 def one_lane_ms(codec, d_in, lane_b, args):
@@ -658,6 +675,7 @@ def main_sharded(args):
     t_max = comm.allreduce_max(elapsed)
     st = shard.stats(args.steps, wall0, wall1)
     summary = dist.combine(comm.allgather_stats(st))
+    ranks = rank_devices(comm, codec, rank, local)
     # the one-lane roofline of the dominant launch group at the shard's batch (as configs[1])
     ms = one_lane_ms(codec, shard.d_img, lane_b, args) if shard.n >= lane_b else None
     roof = None
@@ -699,6 +717,7 @@ def main_sharded(args):
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b},
         "tuning": tuning,
         "shard_upload_s": round(t_gen, 2),
+        "ranks": ranks,
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
                             "raw_bpp": round(summary["bpp"], 4), "per_step_images": summary["images"] // args.steps},
     }
@@ -823,6 +842,7 @@ def main_image(args):
                         bits=NI * npat * eh * ew * ec * args.steps, images=NI * args.steps,
                         t_start=wall0, t_end=wall1)
     summary = dist.combine(comm.allgather_stats(st))
+    ranks = rank_devices(comm, codec, rank, local)
 
     # per-layer HIP-event timing of both networks at their per-launch batch sizes
     ms_c = one_lane_ms(codec, d_pat, lane_b, args)
@@ -875,6 +895,7 @@ def main_image(args):
         "roofline": roof,
         "roofline_step_frac": round(t_min * NI * 1e3 / step_ms, 4),
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "windows_per_launch": win_lane},
+        "ranks": ranks,
         "tuning": tuning,
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
                             "raw_bpp": round(summary["bpp"], 4)},

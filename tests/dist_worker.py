@@ -39,8 +39,9 @@ def main():
     port = int(os.environ["MASTER_PORT"]) + 17
     payload = bytes(range(128)) if comm.rank == 0 else None
     uid = dist.exchange_unique_id(comm.rank, comm.world, payload, "127.0.0.1", port)
+    rows = comm.allgather_f64([comm.rank, 10 + comm.rank, 7.5])  # bench.py's per-rank device record path
     res = {"rank": comm.rank, "summary": dist.combine(stats), "tmax": tmax, "uid_ok": uid == bytes(range(128)),
-           "images": [s.images for s in stats]}
+           "images": [s.images for s in stats], "gather": rows.tolist()}
     with open(f"{out}.{comm.rank}", "w") as f:
         json.dump(res, f)
     comm.barrier()

@@ -64,6 +64,7 @@ def test_gloo_world2_sharded_stats(tmp_path, driver):
     res = [json.load(open(f"{out}.{r}")) for r in range(2)]
     assert res[0]["summary"] == res[1]["summary"]
     assert res[0]["images"] == [4, 3] and all(x["uid_ok"] for x in res) and res[0]["tmax"] == 2.0
+    assert res[0]["gather"] == res[1]["gather"] == [[0, 10, 7.5], [1, 11, 7.5]]
     # single-process reference over the whole set
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
     params = synthetic_params(1)
@@ -112,3 +113,20 @@ def test_unique_id_exchange_world3():
         assert p.exitcode == 0
     assert len(got[0]) == 128 and got[0][:5] == bytes([0, 7, 0, 0, 255])
     assert got[1] == got[0] and got[2] == got[0]
+
+
+def test_deadline_ends_a_stalled_wait():
+    """dist.Deadline: a blocking call (RCCL init, a collective) that does not return in time
+    ends the process with exit code 3 and a message naming the wait — a multi-GPU run with a
+    missing peer fails fast instead of hanging."""
+    code = ("import time\nfrom tf_image_compression_amd import dist\n"
+            "with dist.Deadline('ncclCommInitRank (world 8)', 0.5, rank=5):\n    time.sleep(30)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 3
+    assert "[rank 5] ncclCommInitRank (world 8) did not complete within 0 s" in r.stderr or \
+        "[rank 5] ncclCommInitRank (world 8) did not complete within 1 s" in r.stderr
+    ok = subprocess.run([sys.executable, "-c", "from tf_image_compression_amd import dist\n"
+                         "with dist.Deadline('x', 5.0, rank=0):\n    pass\nprint('done')"],
+                        cwd=ROOT, capture_output=True, text=True, timeout=60, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert ok.returncode == 0 and ok.stdout.strip() == "done"

@@ -1,0 +1,147 @@
+"""Winograd F(4x4,3x3) numerics margin and the paths no other test reaches:
+
+* model_3 at 256x256 with heavier-tailed weights than the He-normal fixtures (Student-t,
+  3 degrees of freedom, scaled to the He variance: rare large taps, as trained filters
+  have), end to end against the oracle under the usual bars; the measured errors are
+  written to gpurun_out/wino4_margin.json for DESIGN.md §4;
+* launch_wino4's split loop (conv3x3_wino4.h: batches past 2^29 floats are launched in
+  parts at pointer offsets), forced by option "wino4_max_n": bit-identical to one launch;
+* tic_autotune_step meeting layers that were never tuned and keep no candidate (the
+  r03 'no kernel for layer decode_2' path): every layer keeps a kernel, results unchanged.
+Reference layers: model_3/model.py:74-147,198-272, basic_block/basic_block.py:74-93."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, structured_patches
+from oracle import tic_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _codec(model_id, P, params=None):
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    params = params if params is not None else synthetic_params(model_id, seed=0)
+    return Codec(model_id, params, SYNTH_MEAN, SYNTH_STD, patch_size=P)
+
+
+def _run(c, x):
+    idx, pre = c.encode(x, return_preact=True)
+    u8, f = c.decode(idx, return_float=True)
+    return idx, pre, u8, f
+
+
+def heavy_tailed_params(model_id, seed=0, df=3.0):
+    """Kernels drawn from Student-t(df) scaled to the He variance 2 / (9 Cin), biases as the
+    fixtures: same activation scale, much heavier tails (kurtosis infinite at df = 3)."""
+    from tf_image_compression_amd.weights import synthetic_params
+    base = synthetic_params(model_id, seed=seed)
+    r = np.random.default_rng(7000 + seed)
+    out = {}
+    for k, v in base.items():
+        if k.endswith("/kernel"):
+            he = float(np.std(v.astype(np.float64)))
+            t = r.standard_t(df, v.shape) / np.sqrt(df / (df - 2.0))
+            out[k] = (t * he).astype(np.float32)
+        else:
+            out[k] = v
+    return out
+
+
+def test_wino4_heavy_tailed_weights_model3_256():
+    from tf_image_compression_amd.weights import SYNTH_MEAN, SYNTH_STD
+    P = 256
+    params = heavy_tailed_params(3)
+    x = structured_patches(2, P, seed=910)
+    rec = {}
+    with _codec(3, P, params) as c:
+        for form in (1, 2):
+            c.set_option("s1_form", form)
+            idx, pre = c.encode(x, return_preact=True)
+            ref_pre, ref_idx = o.encoder(params, SYNTH_MEAN, SYNTH_STD, x, P, 2, 3)
+            scale = max(1.0, float(np.max(np.abs(ref_pre))))
+            pre_err = float(np.max(np.abs(pre - ref_pre))) / scale
+            safe = o.decision_margin(ref_pre, 2) > 1e-5 * scale
+            mism = int(np.count_nonzero((idx != ref_idx) & safe))
+            u8, f = c.decode(idx, return_float=True)
+            ref_f, ref_u8 = o.decoder(params, SYNTH_MEAN, SYNTH_STD, idx, 2, 3)
+            dec_err = float(np.max(np.abs(f - ref_f)))
+            du = np.abs(u8.astype(np.int16) - ref_u8.astype(np.int16))
+            edge = np.abs((ref_f - np.floor(ref_f)) - 0.5) < 1e-2
+            rec[f"s1_form_{form}"] = {"preact_rel_err": pre_err, "symbol_mismatches": mism,
+                                      "decoder_max_abs_err": dec_err, "decoder_bar": 1e-2,
+                                      "u8_off_by_one": int(np.count_nonzero(du)),
+                                      "u8_off_not_at_edge": int(np.count_nonzero((du > 0) & ~edge))}
+            assert pre_err <= 1e-4 and mism == 0
+            assert dec_err <= 1e-2, rec
+            assert int(du.max()) <= 1 and int(np.count_nonzero((du > 0) & ~edge)) == 0
+        c.set_option("s1_form", -1)
+    rec["weights"] = "Student-t(3) scaled to the He variance, seed 0; 2 structured 256x256 patches"
+    d = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, "wino4_margin.json"), "w") as fh:
+            json.dump(rec, fh, indent=1)
+
+
+def test_wino4_launch_split_bit_identical():
+    """model_3 at P = 128 (32x32 and 16x16 residual stages) with 7 patches per launch, the
+    F(4x4,3x3) launches split into parts of 3 (3 + 3 + 1) and of 1: bit-identical to the
+    unsplit launches; the per-layer entry likewise."""
+    with _codec(3, 128) as c:
+        c.set_option("s1_form", 2)
+        c.set_option("chain", 0)
+        c.set_option("streams", 1)
+        assert any("conv3x3_wino4_kernel" in k for k in c.layer_kernels(7))
+        x = structured_patches(7, 128, seed=920)
+        ref = _run(c, x)
+        for m in (3, 1):
+            c.set_option("wino4_max_n", m)
+            got = _run(c, x)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b), m
+        # the per-layer entry (tic_conv3x3_device) through the same split loop
+        r = np.random.default_rng(921)
+        n, H = 5, 32
+        xin = r.standard_normal((n, H, H, 64)).astype(np.float32)
+        k = (r.standard_normal((3, 3, 64, 64)) * 0.06).astype(np.float32)
+        b = (r.standard_normal(64) * 0.05).astype(np.float32)
+        d_in, d_out = c.alloc(xin.nbytes), c.alloc(xin.nbytes)
+        d_in.upload(xin)
+        outs = []
+        for m in (0, 2):
+            c.set_option("wino4_max_n", m)
+            c.conv3x3_device(0, 1, d_in, n, H, H, 64, 64, k, b, None, d_out)
+            outs.append(d_out.download(xin.shape, np.float32))
+        assert np.array_equal(outs[0], outs[1])
+        d_in.free()
+        d_out.free()
+        c.set_option("wino4_max_n", 0)
+        c.set_option("s1_form", -1)
+
+
+def test_autotune_step_untuned_layers_keep_kernels(monkeypatch):
+    """tic_autotune_step with its test hooks: every structural flag flips (the fusions and
+    the chain go off, so their layers run standalone without ever having been tuned) and no
+    per-layer candidate wins; every layer must keep a kernel (the r03 bug left such a layer
+    on a null entry: 'no kernel for layer decode_2') and the results stay bit-identical."""
+    monkeypatch.setenv("TIC_TUNE_STEP_TEST", "flip,nowin")
+    n, P = 8, 64
+    x = structured_patches(n, P, seed=930)
+    with _codec(0, P) as c:
+        c.tuning_import("tic-tuning 1\nflag fuse01 1\nflag fuse_tail 1\nflag chain 1\n")
+        ref = _run(c, x)
+        d_in = c.alloc(x.nbytes)
+        d_in.upload(x)
+        c.autotune_step(d_in, n, rounds=1, reps=1)
+        text = c.tuning_export()
+        for flag in ("fuse01", "fuse_tail", "chain"):
+            assert f"flag {flag} 0" in text, text
+        kern = c.layer_kernels(n // 2)
+        assert all(kern), kern  # nothing fused any more: every layer names its own kernel
+        got = _run(c, x)
+        for a, b in zip(ref, got):
+            assert np.array_equal(a, b)
+        d_in.free()

@@ -124,15 +124,16 @@ def check(rc: int, what: str = "") -> int:
 
 def source_digest() -> str:
     """SHA-256 over the device-kernel sources (csrc/*.hip, csrc/*.h: kernels, launch
-    registries, argument blocks) and the HIP build flags: the stamp that ties a tuning
-    state (tuning.py) or a PMC summary (tools/pmc_summary.py) to the kernels it measured.
-    Host-only sources (tic_runtime.cpp, the range coder) are not part of it: registry
-    indices and per-kernel costs do not depend on them."""
+    registries, argument blocks), the host runtime (csrc/tic_runtime.cpp: the tuning text's
+    key and variant conventions, which candidates each form offers, the lane scheduling —
+    ADVICE r03) and the HIP build flags: the stamp that ties a tuning state (tuning.py) or a
+    PMC summary (tools/pmc_summary.py) to the code it measured.  The range coder and the
+    checkpoint reader are not part of it."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(_HERE, "csrc")
     for name in sorted(os.listdir(csrc)):
-        if name.endswith((".h", ".hip")):
+        if name.endswith((".h", ".hip")) or name == "tic_runtime.cpp":
             h.update(name.encode())
             with open(os.path.join(csrc, name), "rb") as f:
                 h.update(f.read())

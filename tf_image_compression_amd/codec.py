@@ -98,6 +98,7 @@ class Codec:
                       f"tic_set_param({name})")
             check(lib().tic_finalize(h), "tic_finalize")
             self.tuning_source = "runtime defaults"
+            self._auto_tuning = tuning == "auto"
             if tuning == "auto":
                 from . import tuning as _tuning
                 self.tuning_source = _tuning.apply(self)
@@ -193,6 +194,10 @@ class Codec:
 
     def set_option(self, key: str, value: int) -> None:
         check(lib().tic_set_option(self._h, key.encode(), int(value)), f"tic_set_option({key})")
+        if key == "streams" and getattr(self, "_auto_tuning", False):
+            # the shipped entries are keyed by per-launch batch, which the lane count changes
+            from . import tuning as _tuning
+            self.tuning_source = _tuning.reapply_entries(self, int(value))
 
     def stream_ptr(self) -> C.c_void_p:
         s = C.c_void_p()

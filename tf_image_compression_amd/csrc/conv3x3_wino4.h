@@ -1,7 +1,9 @@
 // conv3x3_wino4.h — stride-1 'SAME' 3x3 convolutions as Winograd F(4x4, 3x3) on the matrix
 // cores: the res_block convs of model_3 (basic_block/basic_block.py:74-93, model_3/model.py:
-// 66-150,191-281) and the rmbe net's conv_3/4 (submit/2/rmbe/model.py).  Stride-1 form 2
-// (handle option "s1_form" = 2; conv3x3_wino.h is form 1).
+// 66-150,191-281), the rmbe net's conv_3/4 (submit/2/rmbe/model.py) and model_0/1's 16x16
+// stage (model_0/model.py:98-194: the res-block convs, encode_4 with the quantiser epilogue,
+// decode_4 with the dequantiser table on its input).  Stride-1 form 2 (handle option
+// "s1_form" = 2; conv3x3_wino.h is form 1).
 //
 // Per 4x4 output tile with 6x6 input patch d:  Y = A^T [ U (.) V ] A,  U = G g G^T,
 // V = B^T d B, on the interpolation points (0, 1, -1, 2, -1/2, inf).  A tile costs 36
@@ -100,7 +102,7 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   using G = Wino4Geom<TTY>;
   constexpr int NT = G::NT, TTX = G::TTX, LR = G::LR, LCOL = G::LCOL, HPP = G::HPP;
   static_assert(CIN % 16 == 0 && COUT % 32 == 0, "channels");
-  static_assert(IN == IN_F32 && OUT == OUT_F32, "f32 input and output only (the res-block convs)");
+  static_assert(!(IN == IN_IDX && RES), "the dequantiser layer has no residual");
   constexpr int NTHR = 768;
   constexpr int PS = CIN + 8, KC = CIN / 16, C4 = CIN / 4;
   constexpr int RS = 4 * HPP * PS + G::RPAD;  // floats per staged row
@@ -151,13 +153,20 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   auto issue = [&]() {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.in), (short)0, 0x7fffffff, 0x00020000);
-    const int base = nimg * H * W * CIN;  // float offset of the patch (< 2^31: the workspace chunk)
+    const int base = nimg * H * W * CIN;  // element offset of the patch (< 2^31: the workspace chunk)
     walk([&](int i, int row, int col, int c4) {
       const int iy = oy0 - 1 + row, ix = ox0 - 1 + col;
       const bool in = row < LR && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      const int off = in ? (base + (iy * W + ix) * CIN + c4 * 4) * 4 : 0x7fffffff;
-      const w4u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-      pre[i] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+      if constexpr (IN == IN_F32) {
+        const int off = in ? (base + (iy * W + ix) * CIN + c4 * 4) * 4 : 0x7fffffff;
+        const w4u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        pre[i] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+      } else {  // u8 symbols through the dequantiser table (decode_4); SAME padding is 0, not lut[0]
+        const int off = in ? base + (iy * W + ix) * CIN + c4 * 4 : 0x7fffffff;
+        const unsigned q = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+        pre[i] = in ? f32x4{a.lut[q & 0xff], a.lut[(q >> 8) & 0xff], a.lut[(q >> 16) & 0xff], a.lut[q >> 24]}
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     });
   };
   auto commit = [&]() {
@@ -327,7 +336,15 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
           v.z = __fadd_rn(v.z, rr[ps][ay].z);
           v.w = __fadd_rn(v.w, rr[ps][ay].w);
         }
-        *reinterpret_cast<f32x4*>(a.out + o0[ps] + ay * Wo * COUT) = v;
+        const int o = o0[ps] + ay * Wo * COUT;
+        if constexpr (OUT == OUT_F32) {
+          *reinterpret_cast<f32x4*>(a.out + o) = v;
+        } else {  // encode_4: the optional pre-activation, then the quantiser (conv_out4's)
+          if (a.out) *reinterpret_cast<f32x4*>(a.out + o) = v;
+          const uint32_t qv = quant1(v.x, a.qscale) | (quant1(v.y, a.qscale) << 8) |
+                              (quant1(v.z, a.qscale) << 16) | (quant1(v.w, a.qscale) << 24);
+          *reinterpret_cast<uint32_t*>(a.qout + o) = qv;
+        }
       }
     }
   }
@@ -338,10 +355,13 @@ static void launch_wino4(const ConvArgs& a, int n, hipStream_t s) {
   constexpr int OW = 4 * Wino4Geom<TTY>::TTX, OH = 4 * TTY;
   // the kernel's offsets are 32-bit (input: buffer byte offsets below 2^31, so < 2^29 floats;
   // output: element offsets): launch at most 2^29 floats of either at a time (the codec's
-  // chunks are far below that; the per-layer entry takes any batch)
+  // chunks are far below that; the per-layer entry takes any batch).  A single patch of
+  // 2^29 floats or more cannot run in this form: the runtime never selects it for one
+  // (wino4_fits, tic_runtime.cpp).
   const size_t per = (size_t)a.H * a.W * CIN > (size_t)a.Ho * a.Wo * COUT ? (size_t)a.H * a.W * CIN
                                                                            : (size_t)a.Ho * a.Wo * COUT;
-  const int step = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, (((size_t)1 << 29) - 1) / per));
+  int step = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, (((size_t)1 << 29) - 1) / per));
+  if (a.max_n > 0) step = std::min(step, a.max_n);
   for (int n0 = 0; n0 < n; n0 += step) {
     ConvArgs b = a;
     b.in = reinterpret_cast<const float*>(a.in) + (size_t)n0 * a.H * a.W * CIN;

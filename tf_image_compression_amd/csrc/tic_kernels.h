@@ -27,6 +27,8 @@ struct ConvArgs {
   float qscale;        // Q - 1
   int num_cus;         // compute units (persistent variants size their grid from it)
   int grid_cap;        // > 0: cap on the persistent grid (tests force several tiles per workgroup)
+  int max_n;           // > 0: F(4x4,3x3) launches at most this many patches at a time (tests of
+                       // the launch-split path; 0: split only where 32-bit offsets require it)
 };
 
 struct RgbInArgs {
@@ -122,6 +124,10 @@ struct ChainArgs;
 // over the waves), 3 / 4 = two 256- / 512-thread workgroups per region (output channels split
 // in halves over the workgroups: wino_chain_cs.h)
 bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh);
+// A chain of stride-1 64->64 layers on a map of at most 16x16 in Winograd F(4x4,3x3), four
+// workgroups per patch (one per quarter of the output channels; wino4_pchain.h); false if
+// the geometry or the mode combination is not supported.
+bool launch_wino4_pchain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s);
 
 // Whole-image glue and the symbol histogram (image_ops.hip).
 void launch_tile_reflect(const uint8_t* img, int H, int W, int P, int hn, int wn, uint8_t* out, int num_cus,

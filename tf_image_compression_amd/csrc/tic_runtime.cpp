@@ -174,6 +174,12 @@ int same_pad(int kind, int h) {
 // F(4x4,3x3) (weight source 5), else 0 (direct)
 int entry_form(const tic::ConvEntry& c) { return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : 0); }
 
+// F(4x4,3x3) stages a patch through 32-bit buffer byte offsets: a patch (input or output) of
+// >= 2^29 floats cannot run in that form; every other entry fits any patch.
+bool wino4_fits(const tic::ConvEntry& c, int hg, int wg) {
+  return c.wlds != 5 || (long)hg * wg * std::max(c.cin, c.cout) < (1L << 29);
+}
+
 bool form_match(const tic::ConvEntry& c, int form, int fwl) {
   if (fwl >= 0) return c.wlds == fwl;
   if (c.wlds == 3) return false;  // persistent variants: only by autotune or forced
@@ -208,9 +214,9 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
       if (c.cin != cin || c.cout != cout || c.act != act || c.res != res || c.in != in || c.out != outm) continue;
       if (fth && (c.th != fth || c.nsplit != fns || (fwr > 0 && c.wr != fwr))) continue;
       if (!form_match(c, fm, fwl)) continue;
-      // F(4x4,3x3) stages a patch through 32-bit buffer byte offsets: patches of >= 2^29
-      // floats run the next form (the codec's 256x256 patches are far below)
-      if (c.wlds == 5 && (long)hg * wg * c.cin >= (1L << 29)) continue;
+      // patches too large for F(4x4,3x3)'s 32-bit offsets run the next form (the codec's
+      // 256x256 patches are far below)
+      if (!wino4_fits(c, hg, wg)) continue;
       const int cols = c.wlds == 4 ? 32 * c.wr / (c.th / 2) : (c.wlds == 5 ? 256 / c.th : 16);  // output columns / WG
       const long wgs = (long)((wg + cols - 1) / cols) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
       const long work = (long)c.th * cols * 4 / c.nsplit;  // pixels x channel-fraction per workgroup
@@ -234,7 +240,7 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
 
 // Every compiled tiling of this layer signature within one form (all bit-identical).
 std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, int act, int res, int in, int outm,
-                                                   int form = 0) {
+                                                   int form, int hg, int wg) {
   const tic::ConvEntry* (*regs[3])(int*) = {tic::conv_registry_s1, tic::conv_registry_s2,
                                            tic::conv_registry_t2};
   int cnt = 0;
@@ -245,7 +251,7 @@ std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, 
     if (fm < 0) break;
     for (int i = 0; i < cnt; ++i)
       if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
-          e[i].out == outm && e[i].wlds != 3 && entry_form(e[i]) == fm)
+          e[i].out == outm && e[i].wlds != 3 && entry_form(e[i]) == fm && wino4_fits(e[i], hg, wg))
         out.push_back(&e[i]);
   }
   return out;
@@ -443,6 +449,7 @@ struct tic_handle {
   bool use_graph = false;
   bool fuse01 = false;  // encode_0 -> encode_1 through LDS (enc01_kernel); default: struct_defaults
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
+  int wino4_max_n = 0;   // > 0: F(4x4,3x3) launches split into this many patches (tests of the split path)
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3), 2 F(4x4,3x3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
@@ -594,7 +601,7 @@ int check_chain_error(tic_handle* h) {
     HIP_TRY(hipMemcpy(w, ln.ctl, sizeof w, hipMemcpyDeviceToHost));
     if (w[3]) {
       HIP_TRY(hipMemset(ln.ctl + 3, 0, sizeof(unsigned)));
-      return fail(TIC_EHIP, "wino_chain_kernel: a region hand-off timed out (results of that launch are invalid)");
+      return fail(TIC_EHIP, "chain kernel: a hand-off timed out (results of that launch are invalid)");
     }
   }
   return TIC_OK;
@@ -711,34 +718,45 @@ static bool fuses_tail(const tic_handle* h) {
   return ok && d.kind == K_T2 && d.act == 1 && !d.residual && !(!h->rmbe() && L - 2 == h->n_enc);
 }
 
-// wino_chain_kernel: layers [li, chain_end) run in one launch when the handle's "chain"
-// option is on, the stride-1 form is Winograd (the chain reproduces it bit for bit) and
-// li starts a run of >= 2 stride-1 64->64 layers inside one network half (the encoder's
-// last layer may end a run with the quantiser, the decoder's first may start one with the
-// dequantiser).  Returns li when no chain starts there.
+// Chains: layers [li, chain_end) run in one launch when the handle's "chain" option is on,
+// li starts a run of >= 2 stride-1 64->64 layers inside one network half (the encoder's last
+// layer may end a run with the quantiser, the decoder's first may start one with the
+// dequantiser), and the stride-1 form has a chain kernel that reproduces it bit for bit:
+// F(2x2,3x3) (form 1) -> wino_chain_kernel / wino_chain_cs_kernel (8x8 regions handing
+// borders to their neighbours); F(4x4,3x3) (form 2) on maps of at most 16x16 ->
+// wino4_pchain_kernel (four channel-quarter workgroups per patch, no spatial hand-off).
+// Returns li when no chain starts there.
+static bool pchain_form(const tic_handle* h, int li) { return h->s1_form == 2 && h->layers[li].h_in <= 16; }
 static int chain_end(const tic_handle* h, int li) {
   const int L = (int)h->layers.size();
-  if (!h->chain || h->s1_form != 1 || li == 0 || li >= L - 1) return li;
+  if (!h->chain || li == 0 || li >= L - 1) return li;
+  if (h->s1_form != 1 && !(h->s1_form == 2 && h->layers[li].h_in <= 16)) return li;
   auto s1_64 = [&](int i) {
     const LayerDef& d = h->layers[i].def;
     return d.kind == K_S1 && d.cin == 64 && d.cout == 64 && i > 0 && i < L - 1;
   };
-  if (!s1_64(li)) return li;
-  // Geometry the kernel can run: a region waits for its neighbours, so about rw + 2 regions
-  // of a patch must be resident at once in every lane running a chain (resident slots: one
-  // 512-thread or two 256-thread workgroups per CU; margin 2x), and the hand-off buffer's
-  // byte offsets (n * R * 8 KB, n <= chunk) must fit the 32-bit buffer-resource range.
-  {
-    const int rw = (h->layers[li].h_in + 7) / 8;
-    const int per_region = h->chain_wh >= 3 ? 2 : 1;  // workgroups per region
-    const long slots = (long)h->num_cus * (h->chain_wh == 2 || h->chain_wh == 4 ? 1 : 2);
-    if ((long)h->nlanes * per_region * (2L * rw + 2) > slots) return li;
-    if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
-  }
+  if (!s1_64(li) || h->layers[li].def.residual) return li;
   const bool first_dec = !h->rmbe() && li == h->n_enc;
   if (!first_dec && s1_64(li - 1) && (h->rmbe() || li - 1 != h->n_enc - 1)) return li;  // not a run start
   int j = li + 1;
   while (j < L - 1 && j - li < tic::CH_MAX_LAYERS && s1_64(j) && (h->rmbe() || j != h->n_enc)) ++j;
+  if (h->s1_form == 1) {
+    // Geometry the region chain can run: a region keeps its workgroup for all nl
+    // layers, and to publish layer k region t needs layer k-1 of region t + rw + 1, which needs
+    // layer k-2 of t + 2 (rw + 1) ...: min(R, (nl - 1)(rw + 1) + 1) workgroups of a patch must
+    // be resident together in every lane running a chain (resident slots: one 512-thread or two
+    // 256-thread workgroups per CU; margin 2x).  A run that does not fit is shortened (its
+    // remaining layers run unfused).  And the hand-off buffer's byte offsets (n * R * 8 KB,
+    // n <= chunk) must fit the 32-bit buffer-resource range.
+    const int rw = (h->layers[li].h_in + 7) / 8;
+    const long R = (long)rw * rw;
+    const int per_region = h->chain_wh >= 3 ? 2 : 1;  // workgroups per region
+    const long slots = (long)h->num_cus * (h->chain_wh == 2 || h->chain_wh == 4 ? 1 : 2);
+    auto need = [&](int nl) { return 2L * h->nlanes * per_region * std::min(R, (long)(nl - 1) * (rw + 1) + 1); };
+    while (j - li >= 2 && need(j - li) > slots) --j;
+    if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
+  }
+  // (form 2: four workgroups of a patch wait for each other; one per CU is always resident)
   return j - li >= 2 ? j : li;
 }
 // layer i runs inside some wino_chain_kernel launch
@@ -893,13 +911,16 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
     if (ce > li && ce <= l1) {
       const int nl = ce - li;
       const bool last_enc_c = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      const int R = ((lay.h_in + 7) / 8) * ((lay.h_in + 7) / 8);
+      const bool pc = pchain_form(h, li);
+      // hand-off buffers: 8x8 regions (form 1), or four channel quarters per patch, whose
+      // 16 KB slices take the room of four regions' records
+      const int R = pc ? 4 : ((lay.h_in + 7) / 8) * ((lay.h_in + 7) / 8);
       int rc = ensure_chain(h, ln, nl, n, R);
       if (rc) return rc;
       tic::ChainArgs a{};
       for (int k = 0; k < nl; ++k) {
         const LayerRT& lk = h->layers[li + k];
-        a.layer[k] = {lk.d_ww, lk.d_b, lk.def.act, lk.def.residual};
+        a.layer[k] = {pc ? lk.d_ww4 : lk.d_ww, lk.d_b, lk.def.act, lk.def.residual};
       }
       a.nl = nl;
       a.in = first_dec ? in : (const void*)src;
@@ -916,11 +937,11 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.dispatch_order = h->chain_order;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
-        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R * (h->chain_wh >= 3 ? 2 : 1), st, &a.tstamp);
+        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R * (!pc && h->chain_wh >= 3 ? 2 : 1), st, &a.tstamp);
         if (rc2) return rc2;
       }
-      if (!tic::launch_wino_chain(first_dec ? tic::IN_IDX : tic::IN_F32, last_enc_c ? tic::OUT_QUANT : tic::OUT_F32, a,
-                                  st, h->chain_wh))
+      const int inm = first_dec ? tic::IN_IDX : tic::IN_F32, outm = last_enc_c ? tic::OUT_QUANT : tic::OUT_F32;
+      if (pc ? !tic::launch_wino4_pchain(inm, outm, a, st) : !tic::launch_wino_chain(inm, outm, a, st, h->chain_wh))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);
       rc = check_launch();
       if (rc) return rc;
@@ -995,7 +1016,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       const int hg = d.kind == K_T2 ? lay.h_in : lay.h_out;
       const tic::ConvEntry* e = nullptr;
       auto it = lay.tuned.find(tkey(h, lay, n));
-      if (it != lay.tuned.end()) e = it->second;
+      if (it != lay.tuned.end() && wino4_fits(*it->second, hg, hg)) e = it->second;
       else e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, hg, hg, n, layer_form(h, lay));
       if (!e)
         return fail(TIC_EUNSUPPORTED, "no kernel for layer %s (kind %d %d->%d act %d res %d in %d out %d)",
@@ -1014,9 +1035,10 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.qscale = (float)(h->Q - 1);
       a.num_cus = h->num_cus;
       a.grid_cap = h->persist_grid;
+      a.max_n = h->wino4_max_n;
       if (h->tune_reps > 0 && it == lay.tuned.end()) {
         // time every compiled tiling on the live buffers (re-launching is idempotent)
-        auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, layer_form(h, lay));
+        auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, inm, outm, layer_form(h, lay), hg, hg);
         Event t0, t1;
         HIP_TRY(t0.create());
         HIP_TRY(t1.create());
@@ -1646,6 +1668,12 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->persist_grid = value;
     return TIC_OK;
   }
+  if (k == "wino4_max_n") {  // tests: F(4x4,3x3) launches of at most this many patches (0: no cap)
+    if (value < 0) return fail(TIC_EINVAL, "wino4_max_n must be >= 0");
+    clear_graphs(h);
+    h->wino4_max_n = value;
+    return TIC_OK;
+  }
   if (k == "graph") {
     h->use_graph = value != 0;
     return TIC_OK;
@@ -1937,6 +1965,11 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     return TIC_OK;
   };
   const bool log = getenv("TIC_TUNE_LOG") != nullptr;
+  // test hooks (tests/test_gpu_tuning.py): "flip" accepts every structural alternative (the
+  // fusions and the chain switch state whatever they measure), "nowin" lets no per-layer
+  // candidate win — together they reach layers that were never tuned and keep no candidate
+  const char* tt = getenv("TIC_TUNE_STEP_TEST");
+  const bool t_flip = tt && strstr(tt, "flip"), t_nowin = tt && strstr(tt, "nowin");
   float cur = 0.f;
   rc = measure(&cur);
   if (log && !rc) fprintf(stderr, "tune-step n=%d start: %.2f us\n", n, 1e3f * cur);
@@ -1962,7 +1995,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     *f.v = !was;
     clear_graphs(h);
     float alt = 1e30f;
-    if (f.v == &h->chain && !was && !getenv("TIC_CHAIN_WH")) {
+    if (f.v == &h->chain && !was && !getenv("TIC_CHAIN_WH") && h->s1_form == 1) {
       // switching the chain on: in each of its workgroup shapes (whether it pays depends on
       // the shape: the channel-split ones double the workgroups of small stages)
       const int wh0 = h->chain_wh;
@@ -1984,11 +2017,11 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
       rc = measure(&alt);
       if (log && !rc) fprintf(stderr, "tune-step %s=%d : %.2f us\n", f.name, (int)*f.v, 1e3f * alt);
     }
-    if (!rc && alt < cur) cur = alt;
+    if (!rc && (alt < cur || t_flip)) cur = alt;
     else *f.v = was;
     clear_graphs(h);
   }
-  if (!rc && h->chain && any_chain(h) && !getenv("TIC_CHAIN_WH")) {  // the chain's workgroup shape
+  if (!rc && h->chain && any_chain(h) && !getenv("TIC_CHAIN_WH") && h->s1_form == 1) {  // the region chain's shape
     const int was = h->chain_wh;
     int best_wh = was;
     for (int wh = 1; wh <= 4 && !rc; ++wh) {
@@ -2063,8 +2096,9 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
         cur = best;
       } else {
         const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
+        const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
         auto cands = conv_candidates(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
-                                     last_enc ? tic::OUT_QUANT : tic::OUT_F32, layer_form(h, l));
+                                     last_enc ? tic::OUT_QUANT : tic::OUT_F32, layer_form(h, l), hg, hg);
         // an untuned size runs find_conv's pick: `keep` is then null and, when no candidate beats
         // the current step, the size stays untuned (not a null entry, which would drop the layer)
         auto kt = l.tuned.find(tkey(h, l, sizes[0]));
@@ -2079,7 +2113,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
           if (log)
             fprintf(stderr, "tune-step %-22s th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), c->th, c->nsplit,
                     c->wlds, 1e3f * ms);
-          if (!rc && ms < best) {
+          if (!rc && ms < best && !t_nowin) {
             best = ms;
             best_e = c;
           }
@@ -2116,12 +2150,12 @@ int tic_layer_variant(const tic_handle* h, int i, int n, int* th, int* nsplit) {
   }
   auto it = l.tuned.find(tkey(h, l, n));
   const tic::ConvEntry* e = nullptr;
-  if (it != l.tuned.end()) {
+  const int hg = l.def.kind == K_T2 ? l.h_in : l.h_out;
+  if (it != l.tuned.end() && wino4_fits(*it->second, hg, hg)) {
     e = it->second;
   } else {
     const LayerDef& d = l.def;
     const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
-    const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
     e = find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
                   last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
   }
@@ -2147,7 +2181,9 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     if (cs == i) {
       const int ce = chain_end(h, cs);
       const bool first_dec = !h->rmbe() && cs == h->n_enc, last_enc = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      if (h->chain_wh >= 3)
+      if (pchain_form(h, cs))
+        snprintf(buf, sizeof buf, "wino4_pchain_kernel<%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0);
+      else if (h->chain_wh >= 3)
         snprintf(buf, sizeof buf, "wino_chain_cs_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0,
                  h->chain_wh - 2);
       else
@@ -2187,8 +2223,9 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
     auto it = l.tuned.find(tkey(h, l, n));
     const tic::ConvEntry* e =
-        it != l.tuned.end() ? it->second
-                            : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
+        it != l.tuned.end() && wino4_fits(*it->second, hg, hg)
+            ? it->second
+            : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
                                         last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
     if (e->wlds == 5)
@@ -2278,6 +2315,10 @@ int tic_tuning_import(tic_handle* h, const char* text) {
           ce->res != ld.residual || ce->in != (first_dec ? tic::IN_IDX : tic::IN_F32) ||
           ce->out != (last_enc ? tic::OUT_QUANT : tic::OUT_F32))
         return fail(TIC_EINVAL, "tuning line %d: kernel does not match layer %s", line, ld.name.c_str());
+      const int hg = ld.kind == K_T2 ? h->layers[a].h_in : h->layers[a].h_out;
+      if (!wino4_fits(*ce, hg, hg))
+        return fail(TIC_EINVAL, "tuning line %d: the F(4x4,3x3) form cannot run layer %s at this patch size", line,
+                    ld.name.c_str());
       tuned[a][b] = ce;
     } else if (!strcmp(kind, "var")) {
       if (sscanf(ln.c_str(), "var %d %d %d", &a, &b, &c) != 3 || a < 0 || a >= L || c < 0 || b == 0)
@@ -2347,6 +2388,7 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.pad_x = same_pad(kind, W);
   a.num_cus = h->num_cus;
   a.grid_cap = h->persist_grid;
+  a.max_n = h->wino4_max_n;
   touch(h);
   e->fn(a, n, h->stream);
   int rc = check_launch();
@@ -2374,8 +2416,8 @@ int tic_device_info(tic_handle* h, char* buf, int len) {
   if (!h || !buf || len <= 0) return fail(TIC_EINVAL, "bad arguments");
   hipDeviceProp_t p;
   HIP_TRY(hipGetDeviceProperties(&p, h->device));
-  snprintf(buf, len, "%s | %s | CUs %d | HBM %.1f GB | device %d", p.name, p.gcnArchName, p.multiProcessorCount,
-           p.totalGlobalMem / 1e9, h->device);
+  snprintf(buf, len, "%s | %s | CUs %d | HBM %.1f GB | device %d | pci %04x:%02x:%02x", p.name, p.gcnArchName,
+           p.multiProcessorCount, p.totalGlobalMem / 1e9, h->device, p.pciDomainID, p.pciBusID, p.pciDeviceID);
   return TIC_OK;
 }
 

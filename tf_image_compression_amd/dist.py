@@ -24,6 +24,8 @@ import ctypes as C
 import os
 import socket
 import struct
+import sys
+import threading
 import time
 from dataclasses import dataclass
 
@@ -83,6 +85,36 @@ def env_rank() -> tuple[int, int, int]:
     return rank, world, local
 
 
+class Deadline:
+    """A bounded wait around a blocking call that can hang when a peer never arrives (RCCL
+    communicator creation, a collective and its synchronisation, the id rendezvous): if the
+    call has not returned after `seconds`, say which rank waited for what and end the process
+    with exit code 3 — a clear failure instead of a stalled multi-GPU run (never a re-exec;
+    the GPU is released by the process exit).  TIC_DIST_TIMEOUT overrides the default."""
+
+    def __init__(self, what: str, seconds: float | None = None, rank: int | None = None):
+        self.what = what
+        self.seconds = float(os.environ.get("TIC_DIST_TIMEOUT", seconds if seconds is not None else 120.0))
+        self.rank = env_rank()[0] if rank is None else rank
+        self._timer = None
+
+    def _fire(self):
+        sys.stderr.write(f"[rank {self.rank}] {self.what} did not complete within {self.seconds:.0f} s "
+                         f"(a peer rank is missing or stalled): exiting with code 3\n")
+        sys.stderr.flush()
+        os._exit(3)
+
+    def __enter__(self):
+        self._timer = threading.Timer(self.seconds, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._timer.cancel()
+        return False
+
+
 class LocalComm:
     rank, world = 0, 1
 
@@ -94,6 +126,9 @@ class LocalComm:
 
     def allgather_stats(self, s: RankStats) -> list[RankStats]:
         return [s]
+
+    def allgather_f64(self, a) -> np.ndarray:
+        return np.asarray(a, np.float64).reshape(1, -1)
 
     def close(self):
         pass
@@ -124,6 +159,13 @@ class GlooComm:
         out = [torch.zeros(6, dtype=torch.float64) for _ in range(self.world)]
         self.dist.all_gather(out, t)
         return [RankStats.from_array(o.numpy()) for o in out]
+
+    def allgather_f64(self, a) -> np.ndarray:
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a, np.float64).reshape(-1))
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return np.stack([o.numpy() for o in out])
 
     def close(self):
         self.dist.destroy_process_group()
@@ -213,16 +255,19 @@ class RcclComm:
             self._ok(self.nccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = port or int(os.environ.get("TIC_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 17))
-        raw = exchange_unique_id(rank, world, uid_to_bytes(uid) if rank == 0 else None, addr, port)
+        with Deadline(f"ncclUniqueId rendezvous on {addr}:{port}", 150.0, rank):
+            raw = exchange_unique_id(rank, world, uid_to_bytes(uid) if rank == 0 else None, addr, port)
         uid = uid_from_bytes(raw)
         self.comm = C.c_void_p()
-        self._ok(self.nccl.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
+        with Deadline(f"ncclCommInitRank (world {world})", 120.0, rank):
+            self._ok(self.nccl.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
         self.stream = codec.stream_ptr()
         # every collective below is followed by a synchronisation, so nothing of ours stays
         # pending on the codec's stream: its lanes need not fork from it at every call
         codec.stream_external(False)
-        self.d_send = codec.alloc(8 * 6)
-        self.d_recv = codec.alloc(8 * 6 * world)
+        self.cap = 16  # f64 words per rank a gather carries
+        self.d_send = codec.alloc(8 * self.cap)
+        self.d_recv = codec.alloc(8 * self.cap * world)
 
     def _ok(self, rc, what):
         if rc != 0:
@@ -230,21 +275,29 @@ class RcclComm:
 
     def allreduce_max(self, x: float) -> float:
         self.d_send.upload(np.array([x], np.float64))
-        self._ok(self.nccl.ncclAllReduce(self.d_send.ptr, self.d_recv.ptr, 1, NCCL_FLOAT64, NCCL_MAX, self.comm,
-                                         self.stream), "ncclAllReduce")
-        self.codec.synchronize()
+        with Deadline("ncclAllReduce(max)", 60.0, self.rank):
+            self._ok(self.nccl.ncclAllReduce(self.d_send.ptr, self.d_recv.ptr, 1, NCCL_FLOAT64, NCCL_MAX, self.comm,
+                                             self.stream), "ncclAllReduce")
+            self.codec.synchronize()
         return float(self.d_recv.download((1,), np.float64)[0])
 
     def barrier(self):
         self.allreduce_max(0.0)
 
+    def allgather_f64(self, a) -> np.ndarray:
+        """[world, k] f64: every rank's k words (k <= 16), one ncclAllGather on the codec stream."""
+        a = np.ascontiguousarray(a, np.float64).reshape(-1)
+        if a.size > self.cap:
+            raise ValueError(f"allgather_f64 carries at most {self.cap} words per rank")
+        self.d_send.upload(a)
+        with Deadline("ncclAllGather", 60.0, self.rank):
+            self._ok(self.nccl.ncclAllGather(self.d_send.ptr, self.d_recv.ptr, a.size, NCCL_FLOAT64, self.comm,
+                                             self.stream), "ncclAllGather")
+            self.codec.synchronize()
+        return self.d_recv.download((self.world, a.size), np.float64)
+
     def allgather_stats(self, s: RankStats) -> list[RankStats]:
-        self.d_send.upload(s.to_array())
-        self._ok(self.nccl.ncclAllGather(self.d_send.ptr, self.d_recv.ptr, 6, NCCL_FLOAT64, self.comm, self.stream),
-                 "ncclAllGather")
-        self.codec.synchronize()
-        a = self.d_recv.download((self.world, 6), np.float64)
-        return [RankStats.from_array(r) for r in a]
+        return [RankStats.from_array(r) for r in self.allgather_f64(s.to_array())]
 
     def close(self):
         if self.comm:

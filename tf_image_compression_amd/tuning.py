@@ -87,11 +87,21 @@ def merged_text(docs, with_entries: bool) -> str:
     return "\n".join(lines) + "\n"
 
 
+def env_streams() -> int:
+    """The lane count a new handle starts with: TIC_STREAMS clamped to 1..4 exactly as the
+    runtime clamps it (tic_create), default 2."""
+    try:
+        v = int(os.environ.get("TIC_STREAMS", "2"))
+    except ValueError:
+        v = 2
+    return min(4, max(1, v))
+
+
 def apply(codec, streams: int | None = None) -> str:
     """Apply the shipped tuning matching the codec's (model, patch, lanes); returns a short
     description of what was applied (Codec.tuning_source)."""
     if streams is None:
-        streams = int(os.environ.get("TIC_STREAMS", "2"))
+        streams = env_streams()
     ents = entries(codec.model_id, codec.patch_size, streams)
     if not ents:
         return "runtime defaults (no shipped tuning for this model / patch / lanes)"
@@ -101,3 +111,17 @@ def apply(codec, streams: int | None = None) -> str:
         return "shipped tuning: " + ", ".join(os.path.basename(e[1]) for e in fresh)
     codec.tuning_import(merged_text([e[2] for e in ents], False))
     return "shipped tuning flags only (stamp mismatch): " + os.path.basename(ents[0][1])
+
+
+def reapply_entries(codec, streams: int) -> str:
+    """After the lane count changed (option "streams"): the per-layer entries keyed by the
+    new per-launch batches, from the shipped tuning for (model, P, streams) when its stamp
+    matches — or none — and the structural flags left as they are (entries
+    measured for another lane count no longer match the batches the lanes see)."""
+    ents = [e for e in entries(codec.model_id, codec.patch_size, streams)
+            if e[2].get("_meta", {}).get("source_sha256") == source_digest()]
+    text = merged_text([e[2] for e in ents], True) if ents else "tic-tuning 1\n"
+    text = "\n".join(ln for ln in text.splitlines() if not ln.startswith("flag ")) + "\n"
+    codec.tuning_import(text)
+    return ("shipped tuning entries: " + ", ".join(os.path.basename(e[1]) for e in ents)) if ents else \
+        f"runtime defaults (no shipped tuning for {streams} lanes)"
