@@ -74,6 +74,9 @@ def parse():
                     help="PMC mode (tools/pmc_box.sh): tune exactly as the bench does, then run --steps "
                          "steps on ONE lane at the per-lane batch (deterministic dispatch order), write "
                          "the launch plan of one step to this path, print nothing else")
+    ap.add_argument("--in-step-min", type=int, default=50,
+                    help="at least this many two-lane steps per in-step timing candidate (run before the "
+                         "timed region; they also bring the GPU to its steady clock)")
     ap.add_argument("--layers-out", default=os.path.join(ROOT, "gpurun_out", "bench_layers.json"))
     ap.add_argument("--workload", choices=["patches", "image4k", "sharded"], default="patches",
                     help="patches: BASELINE configs[1]/[2] (default); image4k: configs[4], whole "
@@ -168,6 +171,27 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
         g["launches"] += 1
         i = j + 1
     return groups, rows
+
+
+def kernel_families(groups, kernels, names):
+    """Launch groups merged by kernel template (the instance name up to '<'): the encoder and
+    decoder chain runs are one family, as are the same conv template at two shapes.  The
+    dominant launch is the family with the most one-lane time per step (a tie between two
+    launches of one template, e.g. the two chains at 50.6 / 50.3 us, then cannot flip the pick
+    from run to run — VERDICT r03 item 4); its roofline is over all its launches: the mean
+    FLOPs / bytes per launch over the mean duration."""
+    fams = {}
+    for k, g in groups.items():
+        inst = kernels[names[g["layers"][0]]] if kernels is not None else "+".join(g["layers"])
+        fams.setdefault(inst.split("<")[0], []).append(k)
+    out = {}
+    for fam, members in fams.items():
+        L = sum(groups[k]["launches"] for k in members)
+        mean = lambda f: sum(groups[k][f] * groups[k]["launches"] for k in members) / L
+        out[fam] = {"members": members, "layers": [nm for k in members for nm in groups[k]["layers"]],
+                    "ms": sum(groups[k]["ms"] for k in members), "launches": L,
+                    "flops": mean("flops"), "bytes": mean("bytes"), "wbytes": mean("wbytes")}
+    return out
 
 
 def roofline_of(group, batch):
@@ -391,7 +415,33 @@ def main():
     groups, rows = kernel_groups(codec, M, P, ms, kernels)
     names = {lay.name: i for i, lay in enumerate(layer_table(M))}
     # candidates timed in-step: the four largest by one-lane time per step
-    cands = sorted(groups, key=lambda k: (-groups[k]["ms"], -groups[k]["flops"]))[:4]
+    fams = kernel_families(groups, kernels, names)
+    dom_fam = max(fams, key=lambda f: (fams[f]["ms"], fams[f]["flops"]))
+    cands = list(fams[dom_fam]["members"])
+    cands += [k for k in sorted(groups, key=lambda k: (-groups[k]["ms"], -groups[k]["flops"])) if k not in cands][
+        :max(0, 4 - len(cands))]
+    # the candidates' launches timed in-step, BEFORE the timed region: the same steady two-lane
+    # steps with an event pair per lane around each candidate launch (inside the timed steps the
+    # pairs would cost ≈ 2 %), warm-up steps first to settle the lanes.  Running them here also
+    # brings the GPU to the clock it holds under sustained load: the kernels of a step get
+    # ≈ 7 % faster over the first ≈ 30 steps after the light one-lane profiling (rocprofv3
+    # kernel trace of a 20-step run: step span 411 -> 350 us), which 5 warm-up
+    # steps alone do not cover
+    in_step = {}
+    n_in_step = max(args.in_step_min, min(args.steps, 200))
+    if args.trace_only:  # the same sustained steps, without the event pairs
+        for _ in range(len(cands) * (args.warmup + n_in_step)):
+            codec.codec_device(d_in, B, d_idx, d_rgb)
+    else:
+        for k in cands:
+            codec.set_option("mark_layer", names[groups[k]["layers"][0]])
+            for _ in range(args.warmup):
+                codec.codec_device(d_in, B, d_idx, d_rgb)
+            codec.mark_durations()
+            for _ in range(n_in_step):
+                codec.codec_device(d_in, B, d_idx, d_rgb)
+            in_step[k] = codec.mark_durations()
+        codec.set_option("mark_layer", -1)
     for _ in range(args.warmup):
         codec.codec_device(d_in, B, d_idx, d_rgb)
     codec.synchronize()
@@ -407,22 +457,6 @@ def main():
     elapsed = time.perf_counter() - t0
     wall1 = time.time()
     t_max = comm.allreduce_max(elapsed)
-    # the candidates' launches timed in-step: the same steady two-lane steps right after the
-    # timed region (an event pair per lane around each of its launches would cost the timed
-    # steps ≈ 2 %), warm-up steps first to settle the lanes again; the dominant group is the
-    # one with the most in-step time per step (what rocprofv3 --kernel-trace ranks first)
-    in_step = {}
-    n_in_step = max(1, min(args.steps, 200))
-    if not args.trace_only:
-        for k in cands:
-            codec.set_option("mark_layer", names[groups[k]["layers"][0]])
-            for _ in range(args.warmup):
-                codec.codec_device(d_in, B, d_idx, d_rgb)
-            codec.mark_durations()
-            for _ in range(n_in_step):
-                codec.codec_device(d_in, B, d_idx, d_rgb)
-            in_step[k] = codec.mark_durations()
-        codec.set_option("mark_layer", -1)
     in_step = {k: v for k, v in in_step.items() if len(v)}
     # the dominant launch group: a fixed ranking — the most one-lane (exclusive) GPU time per
     # step (cands[0]).  The in-step ranking is reported beside it but does not choose: with
@@ -430,10 +464,10 @@ def main():
     # it, which moves from run to run (model_0: the encoder chain 54 µs in one run, 75 in the
     # next, enc01 72-73 in both; rocprofv3 averages them within 0.1 %), so an in-step pick
     # named a different kernel on every other run
-    dom_key = cands[0]
+    members = fams[dom_fam]["members"]
     top_in_step = (max(in_step, key=lambda k: float(np.mean(in_step[k])) * groups[k]["launches"])
                    if in_step else None)
-    marks = in_step.get(dom_key, np.zeros(0))
+    marks = np.concatenate([in_step[k] for k in members if k in in_step] or [np.zeros(0)])
     if args.trace_only:
         if rank == 0:
             print(json.dumps({"trace_only": True, "ms_per_step": t_max * 1e3 / args.steps,
@@ -454,31 +488,33 @@ def main():
     # the dominant group's roofline from its one-lane (exclusive) launch duration: a
     # kernel-quality figure; beside it the same launches timed in the steady two-lane steps
     # (sharing the chip with the other lane, as rocprofv3 --kernel-trace sees them there)
-    dom = dict(groups[dom_key])
+    dom = dict(fams[dom_fam])
     roof, dom_ms, dom_flops, dom_bytes = roofline_of(dom, lane_b)
     roof["timing"] = (f"one lane, each launch alone: HIP events per launch, median of {args.profile_passes} "
                       f"passes x {args.profile_iters} iterations")
-    roof["dominant_by"] = ("most one-lane (exclusive) GPU time per step: a fixed ranking; the in-step "
-                           "duration beside it, and the group with the most in-step time per step in "
-                           "most_in_step_time when that is another one")
+    roof["dominant_by"] = ("the kernel template with the most one-lane (exclusive) GPU time per step, over "
+                           "all its launches: a fixed ranking; the in-step duration beside it, and the "
+                           "launch with the most in-step time per step (what rocprofv3 --kernel-trace "
+                           "ranks first) in most_in_step_time when that is another kernel")
     if len(marks):
-        di = dict(groups[dom_key])
+        di = dict(dom)
         di["ms"] = float(np.mean(marks)) * di["launches"]
         ri, rmsi, _, _ = roofline_of(di, lane_b)
         roof["ms_per_launch_in_step"] = round(rmsi, 5)
         roof["frac_in_step"] = ri["frac"]
         roof["timing_in_step"] = (f"HIP events around each of its {len(marks)} launches on the lane streams in "
-                                  f"{n_in_step} two-lane steps run right after the timed region (mean)")
+                                  f"{n_in_step} two-lane steps run right before the timed region (mean)")
     # HBM bytes per launch of the dominant kernel instance from the committed PMC summary
     # (tools/pmc_box.sh + tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
-    dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
-    roof.update(pmc_traffic(traffic_path(args, M, lane_b), launch_units(groups[dom_key]["layers"], kernels, names),
+    dom_kernels = sorted({kernels[names[nm]] for nm in dom["layers"]} - {""})
+    roof.update(pmc_traffic(traffic_path(args, M, lane_b), launch_units(dom["layers"], kernels, names),
                             {"model": M, "patch": P, "lane_batch": lane_b}))
     winograd_note(roof, dom_kernels, dom_flops, dom_ms)
-    roof["kernel"] = "+".join(groups[dom_key]["layers"])
+    roof["kernel"] = " | ".join("+".join(groups[k]["layers"]) for k in members)
     roof["kernel_instance"] = dom_kernels
+    roof["launches_per_step_per_lane"] = dom["launches"]
     roof["ms_per_launch"] = round(dom_ms, 5)
-    if top_in_step is not None and top_in_step != dom_key:  # for the record
+    if top_in_step is not None and top_in_step not in members:  # for the record
         r1, ms1, _, _ = roofline_of(groups[top_in_step], lane_b)
         gi = dict(groups[top_in_step])
         gi["ms"] = float(np.mean(in_step[top_in_step])) * gi["launches"]
@@ -682,15 +718,16 @@ def main_sharded(args):
     if ms is not None:
         kernels = codec.layer_kernels(lane_b)
         groups, _ = kernel_groups(codec, M, P, ms, kernels)
-        dom_key = max(groups, key=lambda k: groups[k]["ms"])
-        roof, dom_ms, dom_flops, _ = roofline_of(groups[dom_key], lane_b)
         from tf_image_compression_amd.topology import layer_table
         names = {lay.name: i for i, lay in enumerate(layer_table(M))}
-        dom_kernels = sorted({kernels[names[nm]] for nm in groups[dom_key]["layers"]} - {""})
+        fams = kernel_families(groups, kernels, names)
+        dom = fams[max(fams, key=lambda f: (fams[f]["ms"], fams[f]["flops"]))]
+        roof, dom_ms, dom_flops, _ = roofline_of(dom, lane_b)
+        dom_kernels = sorted({kernels[names[nm]] for nm in dom["layers"]} - {""})
         winograd_note(roof, dom_kernels, dom_flops, dom_ms)
-        roof.update(pmc_traffic(traffic_path(args, M, lane_b), launch_units(groups[dom_key]["layers"], kernels, names),
+        roof.update(pmc_traffic(traffic_path(args, M, lane_b), launch_units(dom["layers"], kernels, names),
                                 {"model": M, "patch": P, "lane_batch": lane_b}))
-        roof["kernel"] = "+".join(groups[dom_key]["layers"])
+        roof["kernel"] = " | ".join("+".join(groups[k]["layers"]) for k in dom["members"])
         roof["kernel_instance"] = dom_kernels
         roof["ms_per_launch"] = round(dom_ms, 5)
         roof["timing"] = "one-lane per-layer HIP events (profile_layers)"

@@ -197,3 +197,40 @@ def test_bench_groups_chain_runs():
     assert chains[1]["bytes"] == hw + hw * 4      # u8 symbols in, f32 out
     assert all(rows[i]["flops_per_patch"] == work[i][1] * bench.WINO_FRAC for i in range(e0, e0 + 5))
     assert sum(g["launches"] for g in groups.values()) == L - 8
+
+
+def test_bench_dominant_by_kernel_family():
+    """bench.py picks the dominant launch by kernel template over all its launches: the two
+    chain runs (one template, two instances) are one family whose one-lane time is their sum,
+    so a 50.6 / 50.3 us tie between them cannot flip the pick; the family's roofline is the
+    mean FLOPs per launch over the mean duration."""
+    import importlib.util
+    import os
+    import numpy as np
+    from tf_image_compression_amd.topology import layer_table
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    lt = layer_table(0)
+    names = {lay.name: i for i, lay in enumerate(lt)}
+    L = len(lt)
+    kernels = [f"k{i}_kernel<{i}>" for i in range(L)]
+    kernels[2], kernels[3] = "conv3x3_kernel<2,32>", "conv3x3_kernel<2,64>"
+    e0, d0 = names["encode_res_1/conv_0"], names["decode_4"]
+    kernels[e0], kernels[d0] = "wino_chain_kernel<0,1,2>", "wino_chain_kernel<1,0,2>"
+    for i in list(range(e0 + 1, e0 + 5)) + list(range(d0 + 1, d0 + 5)):
+        kernels[i] = ""
+    ms = np.full(L, 0.02)
+    ms[0] = 0.0506  # a single launch slower than either chain launch
+    ms[e0], ms[d0] = 0.0503, 0.0501
+    groups, _ = bench.kernel_groups(None, 0, 256, ms, kernels)
+    fams = bench.kernel_families(groups, kernels, names)
+    dom = max(fams, key=lambda f: (fams[f]["ms"], fams[f]["flops"]))
+    assert dom == "wino_chain_kernel" and fams[dom]["launches"] == 2 and len(fams[dom]["members"]) == 2
+    f = fams[dom]
+    gs = [groups[k] for k in f["members"]]
+    roof, ms_launch, flops, _ = bench.roofline_of(f, 32)
+    assert abs(ms_launch - (0.0503 + 0.0501) / 2) < 1e-12
+    assert abs(flops - 32 * (gs[0]["flops"] + gs[1]["flops"]) / 2) < 1e-3
+    # two instances of another template are one family too (the template name up to '<')
+    assert fams["conv3x3_kernel"]["launches"] == 2 and len(fams) == L - 10
