@@ -74,6 +74,8 @@ def parse():
                     help="PMC mode (tools/pmc_box.sh): tune exactly as the bench does, then run --steps "
                          "steps on ONE lane at the per-lane batch (deterministic dispatch order), write "
                          "the launch plan of one step to this path, print nothing else")
+    ap.add_argument("--preheat-s", type=float, default=3.0,
+                    help="seconds of untimed steps before any measurement (fresh-box clock ramp; 0 = off)")
     ap.add_argument("--in-step-min", type=int, default=50,
                     help="at least this many two-lane steps per in-step timing candidate (run before the "
                          "timed region; they also bring the GPU to its steady clock)")
@@ -410,6 +412,7 @@ def main():
     # (exclusive) — the median of --profile-passes passes; it picks the dominant launch group
     # (the most one-lane time per step) and gives its roofline fraction; the same launches are
     # also timed in-step (below) and reported beside it
+    pre = preheat(args, lambda: codec.codec_device(d_in, B, d_idx, d_rgb), codec.synchronize)
     ms = one_lane_ms(codec, d_in, lane_b, args)
     kernels = codec.layer_kernels(lane_b)
     groups, rows = kernel_groups(codec, M, P, ms, kernels)
@@ -559,6 +562,7 @@ def main():
         "roofline_step_frac": round(step_roofline(rows, B, step_ms), 4),
         "lanes": {"streams": args.streams, "patches_per_launch": lane_b, "hip_graph": bool(args.graph)},
         "host_enqueue_ms_per_step": round(t_enq * 1e3 / args.steps, 4),
+        "preheat": pre,
         "ranks": ranks,
         "tuning": tuning,
         "stats_allgather": {"images": summary["images"], "psnr_db": round(summary["psnr_db"], 3),
@@ -597,6 +601,28 @@ def rank_devices(comm, codec, rank, local):
     rows = comm.allgather_f64([rank, local, dev, dom, bus, fn])
     return [{"rank": int(r[0]), "local_rank": int(r[1]), "device": int(r[2]),
              "pci": f"{int(r[3]):04x}:{int(r[4]):02x}:{int(r[5]):02x}"} for r in rows]
+
+
+def preheat(args, step, sync):
+    """Untimed steps for args.preheat_s seconds before any measurement, in chunks of 10 steps
+    with the time of each chunk kept: on a fresh box the first process's steps run ≈ 7 %
+    slower than the same steps a few seconds later, which the driver's 5 warm-up
+    steps do not cover; the chunk times show the ramp."""
+    out = {"seconds": args.preheat_s, "steps": 0, "ms_per_step_by_chunk": []}
+    if args.preheat_s <= 0:
+        return out
+    sync()
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < args.preheat_s:
+        t = time.perf_counter()
+        for _ in range(10):
+            step()
+        sync()
+        out["ms_per_step_by_chunk"].append(round((time.perf_counter() - t) * 100.0, 4))
+        out["steps"] += 10
+    c = out["ms_per_step_by_chunk"]
+    out["ms_per_step_by_chunk"] = c if len(c) <= 12 else c[:6] + c[-6:]  # first and last chunks
+    return out
 
 
 def one_lane_ms(codec, d_in, lane_b, args):
