@@ -138,6 +138,29 @@ def test_wino4_launch_split_bit_identical():
         c.set_option("s1_form", -1)
 
 
+def test_wino4_launch_split_quant_dequant_layers():
+    """The split loop on the u8-input (decode_4, dequantiser) and u8-output (encode_4,
+    quantiser) F(4x4,3x3) layers of model_0 at P = 64 (its 16x16-stage convs standalone, chain
+    off): parts of 1 and 2 patches step the symbols by bytes, not floats — bit-identical to one
+    launch (the split loop once offset the u8 pointers as floats and never offset the symbol
+    output)."""
+    with _codec(0, 64) as c:
+        c.set_option("s1_form", 2)
+        c.set_option("chain", 0)
+        c.set_option("streams", 1)
+        kern = c.layer_kernels(5)
+        assert sum("conv3x3_wino4_kernel" in k for k in kern) == 10, kern
+        x = structured_patches(5, 64, seed=925)
+        ref = _run(c, x)
+        for m in (2, 1):
+            c.set_option("wino4_max_n", m)
+            got = _run(c, x)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b), m
+        c.set_option("wino4_max_n", 0)
+        c.set_option("s1_form", -1)
+
+
 def test_autotune_step_untuned_layers_keep_kernels(monkeypatch):
     """tic_autotune_step with its test hooks: every structural flag flips (the fusions and
     the chain go off, so their layers run standalone without ever having been tuned) and no

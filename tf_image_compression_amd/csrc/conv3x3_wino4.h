@@ -122,6 +122,21 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   int bx, by, bz;
   xcd_tile(bx, by, bz);
   const int oy0 = by * 4 * TTY, ox0 = bx * 4 * TTX, nimg = bz;
+  // timing probe (tools/wino4_timing.py; null in production): s_memrealtime stamps (100 MHz) —
+  // [0] start, [1] loads issued, [2] staged, [3 + w] wave w's K loop done, [15] exchange done,
+  // [16] end; [17] / [18] s_memtime around wave 0's K loop (the shader clock); [22] / [23] the
+  // CU / XCC the workgroup ran on
+  unsigned long long* const tsp =
+      a.tstamp ? a.tstamp + TIC_W4_TS * (blockIdx.x + gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z))
+               : nullptr;
+  auto stamp = [&](int k) {
+    if (tsp && tid == 0) tsp[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  if (tsp && tid == 0) {
+    tsp[22] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID (CU, SE)
+    tsp[23] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+  }
+  stamp(0);
 
   // ---- stage the input tile (all Cin, columns split by (column mod 4), zero outside the
   // image): global loads into registers, then LDS writes ----
@@ -151,6 +166,7 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   // branch-free: a raw buffer load past num_records returns zeros (the SAME padding and the
   // elements past the tile), so the loads need no control flow around them
   auto issue = [&]() {
+    if (a.probe & 2) return;  // timing probe: no staging loads (results invalid)
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.in), (short)0, 0x7fffffff, 0x00020000);
     const int base = nimg * H * W * CIN;  // element offset of the patch (< 2^31: the workspace chunk)
@@ -203,14 +219,23 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
     return fma4s(ce, d[4], s);
   };
 
-  // ---- A fragments (U) from L2, prefetched PF steps ahead; step s = 6 kc + nu ----
+  // ---- A fragments (U) from L2, prefetched PF steps ahead; step s = 6 kc + nu.  Raw buffer
+  // loads: the descriptor in SGPRs, the lane's byte offset in one VGPR (made opaque after the
+  // staging below, so hipcc does not precompute every step's address), the step as an
+  // immediate offset.  They count on vmcnt only, so the compiler waits for them by count
+  // behind the prefetch — the flat loads of a plain pointer also count on lgkmcnt, and every
+  // wait for the column reads from LDS then drained the weight prefetch too (wave 0's K loop
+  // 8.8 -> 5.9 us, the 64x64 launch 189 -> 172 us: tools/wino4_timing.py) ----
   constexpr int NSTEP = 6 * KC, PF = 2;
-  const float* wl = a.wp + (size_t)6 * xi * KC * 16 * COUT + (size_t)(lg * COUT + co_w + li) * 4;
-  // (made opaque after the staging below: otherwise hipcc computes every step's 64-bit weight
-  // address up front and spills them)
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wp), (short)0, 36 * KC * 16 * COUT * 4, 0x00020000);
+  int wl = ((6 * xi * KC * 16 * COUT) + (lg * COUT + co_w + li) * 4) * 4;  // bytes
   auto wglob = [&](int s, int nb) -> f32x4 {
     const int kc = s / 6, nu = s % 6;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * COUT + nb * 64);
+    // timing probe bit 0: every step reads step 0's fragment (L1-resident; results invalid)
+    const int soff = (a.probe & 1) ? 0 : ((nu * KC + kc) * 16 * COUT + nb * 64) * 4;
+    const w4u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(wrs, wl, soff, 0);
+    return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
   };
   // the output quad of this thread is the same in every pass of the Y phase (768 % Q4 == 0)
   constexpr int Q4 = COUT / 4, NTASK = 4 * NT * Q4;
@@ -219,9 +244,12 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   const f32x4 bb = *reinterpret_cast<const f32x4*>(a.bias + 4 * q);
 
   issue();
+  stamp(1);
   {
     commit();
     __syncthreads();
+    stamp(2);
+    if (tsp && tid == 0) tsp[17] = __builtin_amdgcn_s_memtime();
     asm volatile("" : "+v"(wl));
 
     f32x4 av[PF + 1][NBW];
@@ -272,6 +300,8 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
     }
 
     // ---- T = M A over nu (per wave), exchanged through LDS (the input tile is dead) ----
+    if (tsp && lane == 0) tsp[3 + wave] = __builtin_amdgcn_s_memrealtime();
+    if (tsp && tid == 0) tsp[18] = __builtin_amdgcn_s_memtime();
     __syncthreads();
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
@@ -297,6 +327,7 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
       const int ox = ox0 + 4 * (tile % TTX) + b, oy = oy0 + 4 * (tile / TTX);
       nrow[ps] = (it < NTASK && ox < Wo) ? min(4, Ho - oy) : 0;
       o0[ps] = ((nimg * Ho + oy) * Wo + ox) * COUT + 4 * q;
+      if (a.probe & 4) nrow[ps] = 0;  // timing probe: no residual loads, no stores (results invalid)
       if constexpr (RES) {
 #pragma unroll
         for (int ay = 0; ay < 4; ++ay)
@@ -304,6 +335,7 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
       }
     }
     __syncthreads();
+    stamp(15);
 #pragma unroll
     for (int ps = 0; ps < NPASS; ++ps) {
       const int it = ps * NTHR + tid;
@@ -348,6 +380,7 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
       }
     }
   }
+  stamp(16);
 }
 
 template <int CIN, int COUT, int TTY, int ACT, bool RES, int IN, int OUT>
@@ -364,8 +397,12 @@ static void launch_wino4(const ConvArgs& a, int n, hipStream_t s) {
   if (a.max_n > 0) step = std::min(step, a.max_n);
   for (int n0 = 0; n0 < n; n0 += step) {
     ConvArgs b = a;
-    b.in = reinterpret_cast<const float*>(a.in) + (size_t)n0 * a.H * a.W * CIN;
-    b.out = a.out + (size_t)n0 * a.Ho * a.Wo * COUT;
+    // (the u8 symbols of decode_4 step by bytes, the f32 activations by floats; encode_4's
+    // pre-activation output is optional)
+    if (IN == IN_IDX) b.in = reinterpret_cast<const uint8_t*>(a.in) + (size_t)n0 * a.H * a.W * CIN;
+    else b.in = reinterpret_cast<const float*>(a.in) + (size_t)n0 * a.H * a.W * CIN;
+    b.out = a.out ? a.out + (size_t)n0 * a.Ho * a.Wo * COUT : nullptr;
+    if (a.qout) b.qout = a.qout + (size_t)n0 * a.Ho * a.Wo * COUT;
     if (a.res) b.res = a.res + (size_t)n0 * a.Ho * a.Wo * COUT;
     dim3 grid((a.Wo + OW - 1) / OW, (a.Ho + OH - 1) / OH, std::min(step, n - n0));
     hipLaunchKernelGGL((conv3x3_wino4_kernel<CIN, COUT, TTY, ACT, RES, IN, OUT>), grid, dim3(768), 0, s, b);

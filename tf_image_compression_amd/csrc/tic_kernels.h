@@ -29,7 +29,12 @@ struct ConvArgs {
   int grid_cap;        // > 0: cap on the persistent grid (tests force several tiles per workgroup)
   int max_n;           // > 0: F(4x4,3x3) launches at most this many patches at a time (tests of
                        // the launch-split path; 0: split only where 32-bit offsets require it)
+  unsigned long long* tstamp;  // timing probe (TIC_WINO4_TIMING, per-layer entry only): [workgroup]
+                               // [TIC_W4_TS] s_memrealtime stamps + hardware ids; null: off
+  int probe;                   // timing probe bits (TIC_WINO4_PROBE, per-layer entry only; results
+                               // invalid): 1 weights from one step, 2 no staging loads, 4 no stores
 };
+#define TIC_W4_TS 24
 
 struct RgbInArgs {
   const void* in;      // [N,H,W,3] u8 or f32

@@ -2389,12 +2389,33 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.num_cus = h->num_cus;
   a.grid_cap = h->persist_grid;
   a.max_n = h->wino4_max_n;
+  // timing probe of the F(4x4,3x3) kernel (tools/wino4_timing.py): [workgroup][8] stamps,
+  // appended to the file TIC_WINO4_TIMING names as {grid words, stamps}
+  const char* tpath = e->wlds == 5 ? getenv("TIC_WINO4_TIMING") : nullptr;
+  Scratch s_ts;
+  const size_t nwg = (size_t)n * ((a.Ho + 3) / 4) * ((a.Wo + 3) / 4);  // >= the launch's workgroups
+  if (tpath) {
+    HIP_TRY(s_ts.alloc(nwg * TIC_W4_TS * 8));
+    HIP_TRY(hipMemsetAsync(s_ts.p, 0, nwg * TIC_W4_TS * 8, h->stream));
+    a.tstamp = (unsigned long long*)s_ts.p;
+  }
+  if (const char* pr = e->wlds == 5 ? getenv("TIC_WINO4_PROBE") : nullptr) a.probe = atoi(pr);
   touch(h);
   e->fn(a, n, h->stream);
   int rc = check_launch();
   hipError_t se = hipStreamSynchronize(h->stream);
   if (rc) return rc;
   if (se != hipSuccess) return fail(TIC_EHIP, "conv3x3 sync: %s", hipGetErrorString(se));
+  if (tpath) {
+    std::vector<unsigned long long> t(nwg * TIC_W4_TS);
+    HIP_TRY(hipMemcpy(t.data(), s_ts.p, t.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(tpath, "ab")) {
+      const long long g = (long long)nwg;
+      fwrite(&g, 8, 1, f);
+      fwrite(t.data(), 8, t.size(), f);
+      fclose(f);
+    }
+  }
   return TIC_OK;
 }
 
