@@ -54,10 +54,11 @@ def heavy_tailed_params(model_id, seed=0, df=3.0):
 def test_wino4_heavy_tailed_weights_model3_256():
     """Every stride-1 form on the same heavy-tailed weights.  Bars: the north-star ones for
     every form (symbols bit-exact outside the band, u8 within 1 and only at .5 edges, dataset
-    PSNR within 0.02 dB) and the float decoder bar — 1e-2 on [0,255] for the direct and
-    F(2x2,3x3) forms; F(4x4,3x3)'s larger transform constants put it at about twice F(2x2)'s
-    error on these weights (1.3e-2 measured in round 4), so its float bar here is
-    2e-2 and at most 3x the F(2x2,3x3) error on the same weights."""
+    PSNR within 0.02 dB) and a float decoder bar relative to the direct form's own f32 error on
+    these weights: with Student-t(3) taps even the direct form (the reference's op order in
+    f32) reaches 9.6e-3 of the f64 oracle on [0,255] (round 4: direct 9.6e-3, F(2x2,3x3)
+    6.8e-3, F(4x4,3x3) 1.3e-2), so the He-normal fixtures' 1e-2 bar is no margin
+    statement here — each Winograd form must stay within 2x the direct form's error and 2e-2."""
     from tf_image_compression_amd.weights import SYNTH_MEAN, SYNTH_STD
     P = 256
     params = heavy_tailed_params(3)
@@ -96,10 +97,11 @@ def test_wino4_heavy_tailed_weights_model3_256():
         assert r["preact_rel_err"] <= 1e-4 and r["symbol_mismatches"] == 0, rec
         assert r["u8_max_diff"] <= 1 and r["u8_off_not_at_edge"] == 0, rec
         assert r["delta_psnr_db"] <= 0.02, rec
-    assert rec["s1_form_0"]["decoder_max_abs_err"] <= 1e-2, rec
-    assert rec["s1_form_1"]["decoder_max_abs_err"] <= 1e-2, rec
-    e2 = rec["s1_form_2"]["decoder_max_abs_err"]
-    assert e2 <= 2e-2 and e2 <= 3 * max(rec["s1_form_1"]["decoder_max_abs_err"], 1e-3), rec
+    e0 = max(rec["s1_form_0"]["decoder_max_abs_err"], 1e-3)
+    assert e0 <= 2e-2, rec
+    for form in (1, 2):
+        e = rec[f"s1_form_{form}"]["decoder_max_abs_err"]
+        assert e <= 2e-2 and e <= 2 * e0, rec
 
 
 def test_wino4_launch_split_bit_identical():
