@@ -187,3 +187,35 @@ def test_chain_declined_where_geometry_cannot_run():
         assert "wino_chain_kernel" in _kernels_of(c, 32)
         c.set_option("chunk", 100_000)  # n * R * 8 KB > 2^31 - 1 for the largest launch
         assert "wino_chain_kernel" not in _kernels_of(c, 32)
+
+
+def test_chain_shortened_where_a_long_run_cannot_be_resident():
+    """a region keeps its workgroup for all nl layers and publishing
+    layer k of region t waits on region t + rw + 1 (and so on), so min(R, (nl - 1)(rw + 1) + 1)
+    workgroups of a patch must be resident in every lane.  model_0 at P = 4096 (a 256x256
+    stage, rw = 32) fits two-layer runs (2 lanes x 34 regions) but not the 5-layer ones the
+    old rw + 2 guard accepted (2 x 133 > 256 slots): every chain launch covers at most two
+    layers, and the shortened chains run to the unfused launches' exact results."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    P = 4096
+    with Codec(0, synthetic_params(0), SYNTH_MEAN, SYNTH_STD, patch_size=P, tuning="none") as c:
+        c.set_option("s1_form", 1)
+        c.set_option("chain", 1)
+        kern = c.layer_kernels(1)
+        starts = [i for i, k in enumerate(kern) if k.startswith("wino_chain_kernel")]
+        assert starts, kern
+        for i in starts:  # a run = the chain launch + the '' entries of the layers inside it
+            j = i + 1
+            while j < len(kern) and kern[j] == "":
+                j += 1
+            assert j - i <= 2, (i, kern)
+        x = np.random.default_rng(4096).integers(0, 256, (1, P, P, 3), dtype=np.uint8)
+        idx, pre = c.encode(x, return_preact=True)
+        rgb = c.decode(idx)
+        c.set_option("chain", 0)
+        idx0, pre0 = c.encode(x, return_preact=True)
+        rgb0 = c.decode(idx0)
+        assert np.array_equal(pre, pre0) and np.array_equal(idx, idx0) and np.array_equal(rgb, rgb0)
+        c.set_option("chain", -1)
+        c.set_option("s1_form", -1)
