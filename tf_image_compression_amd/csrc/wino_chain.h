@@ -138,18 +138,31 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   const int ry = reg / a.rw, rx = reg % a.rw;
   const int oy0 = ry * 8, ox0 = rx * 8;
 
-  // ---- weights of layer l, step s = 4 kc + nu, straight from L2, prefetched PF ahead ----
+  // ---- weights of layer l, step s = 4 kc + nu, straight from L2, prefetched PF ahead:
+  // raw buffer loads — the layer's descriptor in SGPRs, this lane's byte offset in one VGPR
+  // (the same for every layer), the step as an immediate offset — instead of a 64-bit
+  // address per load (54 v_lshl_add_u64 per layer; at f32 every VALU instruction costs
+  // matrix-pipe time, §3 of DESIGN.md) ----
   constexpr int NSTEP = 4 * KC, PF = 3, NBW = 4 / WH;
   f32x4 av[PF + 1][NBW];
-  auto wglob = [&](int l, int s, int nb) -> f32x4 {
-    const int kc = s >> 2, nu = s & 3;
-    const float* wl = a.layer[l].wu + (size_t)xi * 64 * KC * C + (size_t)(lg * C + li) * 4;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(nu * KC + kc) * 16 * C + (wh * NBW + nb) * 64);
+  const int wlane = ((xi * 64 * KC * C) + (lg * C + li) * 4) * 4;  // bytes
+  auto wsrc = [&](int l) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.layer[l].wu), (short)0, 16 * KC * 16 * C * 4,
+                                             0x00020000);
   };
+  auto wglob = [&](const __amdgpu_buffer_rsrc_t& r, int s, int nb) -> f32x4 {
+    const int kc = s >> 2, nu = s & 3;
+    const u32x4 u =
+        __builtin_amdgcn_raw_buffer_load_b128(r, wlane, ((nu * KC + kc) * 16 * C + (wh * NBW + nb) * 64) * 4, 0);
+    return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+  };
+  {
+    const __amdgpu_buffer_rsrc_t w0 = wsrc(0);
 #pragma unroll
-  for (int p = 0; p < PF; ++p)
+    for (int p = 0; p < PF; ++p)
 #pragma unroll
-    for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(0, p, nb);
+      for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(w0, p, nb);
+  }
 
   // ---- stage the first layer's input tile (zero outside the image = SAME padding) ----
   // The first layer's tile is the res_block input when the chain starts a block, so it
@@ -196,6 +209,8 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   // B^T row xi from input rows iA, iB of each tile (conv3x3_wino_kernel's exact signs)
   const int iA = xi == 0 ? 0 : 1, iB = xi == 3 ? 3 : 2;
   const float sA = xi == 2 ? -1.f : 1.f, sB = (xi == 0 || xi == 3) ? -1.f : 1.f;
+  // (sA, sB) = (+, -) rows 0 / 3, (+, +) row 1, (-, +) row 2
+  const int sgn = __builtin_amdgcn_readfirstlane(sA < 0.f ? 2 : (sB > 0.f ? 1 : 0));
   const int ty_l = li / TTX, tx_l = li % TTX;
   const int offA = ((2 * ty_l + iA) * RP + tx_l) * PS + lg * 4;
   const int offB = ((2 * ty_l + iB) * RP + tx_l) * PS + lg * 4;
@@ -248,6 +263,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     float* const rsd = dst;                              // res layers: the block input tile
     const int ts = 2 + 6 * l;
     stamp(ts);
+    const __amdgpu_buffer_rsrc_t wl = wsrc(l);
 
     // ---- K loop: conv3x3_wino_kernel's order ----
     f32x4 d[2][4];
@@ -262,8 +278,19 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     f32x4 V[4];
     auto transform = [&]() {
       f32x4 r[4];
+      // sA, sB = +-1: sA d0 + sB d1 is one rounded add / subtract (the products are exact),
+      // so the three sign patterns are spelled out (wave-uniform branch): 4 instead of 8
+      // VALU per 4-channel column
+      if (sgn == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = sA * d[0][j] + sB * d[1][j];
+        for (int j = 0; j < 4; ++j) r[j] = d[0][j] - d[1][j];
+      } else if (sgn == 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = d[0][j] + d[1][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = d[1][j] - d[0][j];
+      }
       V[0] = r[0] - r[2];
       V[1] = r[1] + r[2];
       V[2] = r[2] - r[1];
@@ -285,7 +312,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         const int s = kc * 4 + nu;
         if (s + PF < NSTEP) {
 #pragma unroll
-          for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(l, s + PF, nb);
+          for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(wl, s + PF, nb);
         }
         // keep each weight load PF steps (48 MFMAs) ahead of its use: without the fence the
         // scheduler sinks the loads next to their consumers inside the chunk
@@ -301,10 +328,11 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     }
     // the next layer's first weight steps fly during this layer's epilogue and hand-off
     if (!last) {
+      const __amdgpu_buffer_rsrc_t wn = wsrc(l + 1);
 #pragma unroll
       for (int p = 0; p < PF; ++p)
 #pragma unroll
-        for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(l + 1, p, nb);
+        for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(wn, p, nb);
     }
 
     stamp(ts + 1);
