@@ -37,6 +37,20 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Packed-weight fragment loads through a raw buffer resource: the descriptor lives in SGPRs,
+// the lane's byte offset in one VGPR and the K step's byte offset in the instruction's
+// soffset / immediate — no 64-bit address add per load. At f32 MFMA every VALU instruction
+// adds to the matrix time of the SIMD (probe_mfma_valu_r04.txt), so the
+// address math the pointer form needs per load is paid in MFMA throughput.
+typedef unsigned int wu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t weight_rsrc(const float* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 weight_frag(__amdgpu_buffer_rsrc_t r, int lane_byte, int step_byte) {
+  const wu32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, lane_byte, step_byte, 0);
+  return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+}
+
 // XCD-aware block order (MI355X_MICROARCH.md: blocks b and b + 8 are dealt to one XCD):
 // logical tile b' = (b % 8) * (N / 8) + b / 8, so each XCD walks a contiguous run of tiles —
 // x fastest, then the next tile row — and a tile's halo rows, which the tile above read a
@@ -139,10 +153,11 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
       }
     }
   };
-  const float* __restrict__ wl = a.wp + (size_t)(lg * COUT + co_wg + co_wave + li) * 4;
+  const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(a.wp, 9 * CIN * COUT * 4);
+  const int wlb = (lg * COUT + co_wg + co_wave + li) * 16;  // lane byte offset
   auto wglob = [&](int s, int nb) -> f32x4 {
     const int tap = s / KC, kc = s % KC;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC + kc) * 4 * COUT * 4 + nb * 64);
+    return weight_frag(wrs, wlb, ((tap * KC + kc) * 4 * COUT * 4 + nb * 64) * 4);
   };
 
   constexpr int PF = WSRC == 2 ? 6 : 2;  // register prefetch distance (L2 sources)
@@ -717,10 +732,11 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   constexpr int PF = 2, NSTEP = 9 * KC1;
   const int wr = wave / WC, wc = wave % WC;
   const int co_wave = wc * NB1 * 16;
-  const float* __restrict__ wl = a.wp1 + (size_t)(lg * C1 + co_wave + li) * 4;
+  const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(a.wp1, 9 * 16 * KC1 * C1 * 4);
+  const int wlb = (lg * C1 + co_wave + li) * 16;  // lane byte offset
   auto wglob = [&](int s, int nb) -> f32x4 {
     const int tap = s / KC1, kc = s % KC1;
-    return *reinterpret_cast<const f32x4*>(wl + (size_t)(tap * KC1 + kc) * 4 * C1 * 4 + nb * 64);
+    return weight_frag(wrs, wlb, ((tap * KC1 + kc) * 4 * C1 * 4 + nb * 64) * 4);
   };
   f32x4 av[PF + 1][NB1];
 #pragma unroll

@@ -68,9 +68,11 @@ struct Dec10 {
   }
 
   __device__ __forceinline__ static f32x4 wglob(const Dec10Args& a, int s, int nb, int li, int lg) {
+    // raw buffer load (conv3x3.h weight_frag): descriptor and lane offset are loop-invariant
+    // and CSE'd across the unrolled steps; the step offset is a constant
     const int tap = s / KC, kc = s % KC;
-    return *reinterpret_cast<const f32x4*>(a.wp1 + (size_t)(lg * C0 + li) * 4 + (size_t)(tap * KC + kc) * 4 * C0 * 4 +
-                                           nb * 64);
+    return weight_frag(weight_rsrc(a.wp1, 9 * C1 * C0 * 4), (lg * C0 + li) * 16,
+                       ((tap * KC + kc) * 4 * C0 * 4 + nb * 64) * 4);
   }
 
   // decode_1's input rows m0-1 .. m0+3, columns q0-1 .. q0+15 (zero outside) into registers
