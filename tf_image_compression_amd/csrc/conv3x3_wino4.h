@@ -90,10 +90,10 @@ template <int TTY>
 struct Wino4Geom {
   static constexpr int NT = 16;              // 4x4 output tiles per workgroup
   static constexpr int TTX = NT / TTY;       // tiles per tile row
-  static constexpr int LR = 4 * TTY + 2;     // staged input rows
+  static constexpr int LR = 6 * TTY;         // staged rows: the six rows of B^T d per tile row
   static constexpr int LCOL = 4 * TTX + 2;   // staged input columns
   static constexpr int HPP = TTX + 1;        // pixels per (column mod 4) plane
-  static constexpr int RPAD = TTY == 4 ? 8 : 0;
+  static constexpr int RPAD = TTY == 4 ? 16 : 0;  // conflict-free ds_read_b128 (lane groups)
 };
 
 // Weights (ConvArgs::wp): U packed [36 p][Cin/16][4 g][Cout][4 t], p = 6 xi + nu.
@@ -138,13 +138,19 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
   }
   stamp(0);
 
-  // ---- stage the input tile (all Cin, columns split by (column mod 4), zero outside the
-  // image): global loads into registers, then LDS writes ----
-  constexpr int NSTAGE = LR * LCOL * C4;
+  // ---- stage the row half of the input transform, B^T d, for every tile row (all Cin,
+  // columns split by (column mod 4), zero outside the image = SAME pad).  Task = (tile row
+  // ty, staged column col, channel quad c4): the column's six input rows 4 ty .. 4 ty + 5
+  // into registers, then its six rows of B^T d (w4_bt, the factored form the column half
+  // uses too) into LDS rows 6 ty .. 6 ty + 5.  Every wave then reads the one row xi it
+  // needs per column — the row combination is done once per (column, channel), not once
+  // per wave and tile (the two channel-half waves of a row and the two tiles sharing a
+  // column each repeated it: 5.5x the VALU, which at f32 adds to the MFMA time) ----
+  constexpr int NSTAGE = TTY * LCOL * C4;
   constexpr int NIT = (NSTAGE + NTHR - 1) / NTHR;
-  f32x4 pre[NIT];
-  // element i of this thread: channel quad c4 = tid % C4 (C4 divides NTHR), pixel
-  // tid / C4 + i NTHR / C4 of the tile, walked incrementally (row, col) — no divisions
+  f32x4 pre[NIT][6];
+  // task i of this thread: channel quad c4 = tid % C4 (C4 divides NTHR), column
+  // tid / C4 + i NTHR / C4 of the tile rows, walked incrementally (ty, col) — no divisions
   static_assert(NTHR % C4 == 0, "channel quad per thread");
   constexpr int DP = NTHR / C4, DR = DP / LCOL, DC = DP % LCOL;
   auto walk = [&](auto&& fn) {
@@ -170,53 +176,44 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.in), (short)0, 0x7fffffff, 0x00020000);
     const int base = nimg * H * W * CIN;  // element offset of the patch (< 2^31: the workspace chunk)
-    walk([&](int i, int row, int col, int c4) {
-      const int iy = oy0 - 1 + row, ix = ox0 - 1 + col;
-      const bool in = row < LR && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      if constexpr (IN == IN_F32) {
-        const int off = in ? (base + (iy * W + ix) * CIN + c4 * 4) * 4 : 0x7fffffff;
-        const w4u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-        pre[i] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
-      } else {  // u8 symbols through the dequantiser table (decode_4); SAME padding is 0, not lut[0]
-        const int off = in ? base + (iy * W + ix) * CIN + c4 * 4 : 0x7fffffff;
-        const unsigned q = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-        pre[i] = in ? f32x4{a.lut[q & 0xff], a.lut[(q >> 8) & 0xff], a.lut[(q >> 16) & 0xff], a.lut[q >> 24]}
-                    : f32x4{0.f, 0.f, 0.f, 0.f};
+    walk([&](int i, int ty, int col, int c4) {
+      // the last pass's tasks past the tile rows issue nothing (their waves skip the loads)
+      if (!(NSTAGE % NTHR == 0 || i + 1 < NIT || ty < TTY)) return;
+      const int ix = ox0 - 1 + col;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const int iy = oy0 - 1 + 4 * ty + r;
+        const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        if constexpr (IN == IN_F32) {
+          const int off = in ? (base + (iy * W + ix) * CIN + c4 * 4) * 4 : 0x7fffffff;
+          const w4u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+          pre[i][r] = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+        } else {  // u8 symbols through the dequantiser table (decode_4); SAME padding is 0, not lut[0]
+          const int off = in ? base + (iy * W + ix) * CIN + c4 * 4 : 0x7fffffff;
+          const unsigned q = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+          pre[i][r] = in ? f32x4{a.lut[q & 0xff], a.lut[(q >> 8) & 0xff], a.lut[(q >> 16) & 0xff], a.lut[q >> 24]}
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
     });
   };
   auto commit = [&]() {
-    walk([&](int i, int row, int col, int c4) {
-      if ((NSTAGE % NTHR == 0 || i + 1 < NIT) || row < LR)
-        *reinterpret_cast<f32x4*>(&smem[row * RS + ((col & 3) * HPP + (col >> 2)) * PS + c4 * 4]) = pre[i];
+    walk([&](int i, int ty, int col, int c4) {
+      if ((NSTAGE % NTHR == 0 || i + 1 < NIT) || ty < TTY) {
+        f32x4 bt[6];
+        w4_bt(pre[i], bt);
+        float* const dst = &smem[6 * ty * RS + ((col & 3) * HPP + (col >> 2)) * PS + c4 * 4];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) *reinterpret_cast<f32x4*>(dst + r * RS) = bt[r];
+      }
     });
   };
 
-  // ---- row xi of B^T d for tile li: r_j = sum_i BT[xi][i] d[i][j] over the non-zero i ----
+  // ---- row xi of B^T d for tile li, column j, chunk kc: one staged value ----
   const int ty = li / TTX, tx = li % TTX;
-  const int tbase = (4 * ty) * RS + tx * PS + lg * 4;
-  // the fifth non-zero of row xi: BT[0][0] = BT[5][5] = 1
-  const int re = xi == 5 ? 5 : 0;
-  const float c1 = kW4BT[xi][1], c2 = kW4BT[xi][2], c3 = kW4BT[xi][3], c4 = kW4BT[xi][4];
-  // rows 1-4 add 0 x row 0: branch-free (a wave-uniform branch here makes hipcc spill)
-  const float ce = (xi == 0 || xi == 5) ? 1.f : 0.f;
-  auto ld = [&](int i, int j, int kc) -> f32x4 {
-    return *reinterpret_cast<const f32x4*>(&smem[tbase + i * RS + ((j & 3) * HPP + (j >> 2)) * PS + kc * 16]);
-  };
-  // column j of that row for chunk kc, in the operation order c1 d1 + c2 d2 + c3 d3 + c4 d4 + ce de
-  auto ldcol = [&](int j, int kc, f32x4 (&d)[5]) {
-    d[0] = ld(1, j, kc);
-    d[1] = ld(2, j, kc);
-    d[2] = ld(3, j, kc);
-    d[3] = ld(4, j, kc);
-    d[4] = ld(re, j, kc);
-  };
-  auto rcol = [&](const f32x4 (&d)[5]) {
-    f32x4 s = c1 * d[0];
-    s = fma4s(c2, d[1], s);
-    s = fma4s(c3, d[2], s);
-    s = fma4s(c4, d[3], s);
-    return fma4s(ce, d[4], s);
+  const int tbase = (6 * ty + xi) * RS + tx * PS + lg * 4;
+  auto ld = [&](int j, int kc) -> f32x4 {
+    return *reinterpret_cast<const f32x4*>(&smem[tbase + ((j & 3) * HPP + (j >> 2)) * PS + kc * 16]);
   };
 
   // ---- A fragments (U) from L2, prefetched PF steps ahead; step s = 6 kc + nu.  Raw buffer
@@ -259,12 +256,9 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
       for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(p, nb);
     f32x4 V[6];
     {
-      f32x4 r[6], d[5];
+      f32x4 r[6];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        ldcol(j, 0, d);
-        r[j] = rcol(d);
-      }
+      for (int j = 0; j < 6; ++j) r[j] = ld(j, 0);
       w4_bt(r, V);
     }
     f32x4 acc[6][NBW];
@@ -273,13 +267,12 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // Software pipeline: while the MFMAs of point nu of chunk kc issue, column nu of chunk
-    // kc + 1 is read (before them) and combined (after them); the six V of chunk kc + 1
-    // follow the chunk.
+      // Software pipeline: while the MFMAs of point nu of chunk kc issue, column nu of chunk
+    // kc + 1 is read (before them); the six V of chunk kc + 1 follow the chunk.
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const bool next = kc + 1 < KC;
-      f32x4 rn[6], dn[5];
+      f32x4 rn[6];
 #pragma unroll
       for (int nu = 0; nu < 6; ++nu) {
         const int s = kc * 6 + nu;
@@ -287,14 +280,13 @@ __global__ void __launch_bounds__(768) conv3x3_wino4_kernel(const ConvArgs a) {
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
         }
-        if (next) ldcol(nu, kc + 1, dn);
+        if (next) rn[nu] = ld(nu, kc + 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb) acc[nu][nb] = mfma4(av[s % (PF + 1)][nb][tt], V[nu][tt], acc[nu][nb]);
         __builtin_amdgcn_sched_barrier(0);
-        if (next) rn[nu] = rcol(dn);
       }
       if (next) w4_bt(rn, V);
     }

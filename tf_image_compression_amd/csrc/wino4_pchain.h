@@ -15,14 +15,16 @@
 // hand-off table, row 1).  The res_block input a conv_1 adds is held in registers by the
 // thread that computed it (the epilogue mapping is the same in every layer).
 //
-// Waves: 6 (384 threads), wave xi = row xi of B^T: it forms row xi of B^T d for its lane's
-// tile and channel quad, the six column combinations V_(xi, nu) in registers, and runs the six
-// point GEMMs (M = 16 output channels, N = 16 tiles, K = 64) as 6 x 16 v_mfma_f32_16x16x4_f32
-// per layer, issued (tt, nu)-major so consecutive MFMAs use different accumulators.  Every
-// accumulator still sums in the standalone kernel's order (16-channel chunk kc, then t), the
-// transforms are the same functions (w4_bt / w4_at, conv3x3_wino4.h) and the epilogue the same
+// Waves: 6 (384 threads), wave xi = row xi of B^T: it reads row xi of B^T d for its lane's
+// tile and channel quad (staged once per layer, as conv3x3_wino4_kernel stages it: a pass over
+// (tile row, column, channel quad) turns the layer's 18x18 input into the 24 rows of B^T d),
+// forms the six column combinations V_(xi, nu) in registers, and runs the six point GEMMs
+// (M = 16 output channels, N = 16 tiles, K = 64) as 6 x 16 v_mfma_f32_16x16x4_f32 per layer,
+// issued (tt, nu)-major so consecutive MFMAs use different accumulators.  Every accumulator
+// still sums in the standalone kernel's order (16-channel chunk kc, then t), the transforms
+// are the same functions (w4_bt / w4_at, conv3x3_wino4.h) and the epilogue the same
 // operations, so every layer is bit-identical to its conv3x3_wino4_kernel launch
-// (tests/test_gpu_chain.py).
+// (tests/test_gpu_pchain.py).
 //
 // Progress: the four quarters of a patch wait for each other, so they must be co-resident;
 // work is handed out by an atomic ticket (wino_chain.h: at most the last patch is incomplete
@@ -38,18 +40,28 @@ namespace tic {
 namespace pchain {
 constexpr int C = 64, KC = 4;
 constexpr int NT = 16, TTX = 4, LR = 18, LCOL = 18, HPP = 5, PS = 72;
-constexpr int RS = 4 * HPP * PS + 8;  // floats per staged row (conv3x3_wino4_kernel, TTY = 4)
-constexpr int TILE = LR * RS;         // 26064 floats = 104 KB
+constexpr int RS = 4 * HPP * PS + 16;  // floats per staged row (conv3x3_wino4_kernel, TTY = 4)
+constexpr int LT = 24;                 // rows of B^T d: six per tile row
+constexpr int TILE = LT * RS;          // 34944 floats = 137 KB; the raw 18x18 input (rows
+                                       // 0..17, same pitch) and the T exchange alias it
 constexpr int CQ = 16;                // output channels per workgroup
 constexpr int XS = CQ + 4;            // T-exchange pitch per (xi, b, tile)
 constexpr int XCH = 24 * NT * XS;     // 7680 floats: aliases rows 0..5 of the (dead) tile
-constexpr int XROWS = (XCH + RS - 1) / RS;
 constexpr int NTH = 384;
 constexpr int SLICE = 256 * CQ;  // floats a workgroup publishes per layer: [256 px][16 ch]
-static_assert(XROWS <= 6, "the ring re-zeroing below covers rows 0..5");
+constexpr int NBT = 4 * LCOL * 16 / NTH;  // B^T d tasks (tile row, column, quad) per thread: 3
+static_assert(NBT * NTH == 4 * LCOL * 16, "B^T d tasks split evenly");
 
-// LDS float offset of staged pixel (row, col) of the 18x18 tile (columns split by col mod 4)
+// LDS float offset of staged pixel (row, col) of the 18x18 tile (columns split by col mod 4);
+// row 6 ty + xi of the B^T d rows uses the same column layout
 __device__ __forceinline__ int tpix(int row, int col) { return row * RS + ((col & 3) * HPP + (col >> 2)) * PS; }
+// B^T d task k of thread t: (tile row, column, channel quad)
+__device__ __forceinline__ void bt_task(int t, int k, int& ty, int& col, int& c4) {
+  const int e = k * NTH + t, p = e >> 4;
+  c4 = e & 15;
+  ty = p / LCOL;
+  col = p - ty * LCOL;
+}
 }  // namespace pchain
 
 // IN: IN_F32 / IN_IDX for the first layer; OUT: OUT_F32 / OUT_QUANT for the last one.
@@ -112,22 +124,28 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
     }
   };
 
-  // ---- stage the first layer's input: all 64 channels, 18x18 with the zero ring ----
-  {
-    constexpr int NSTAGE = LR * LCOL * (C / 4);
-    constexpr int NIT = (NSTAGE + NTH - 1) / NTH;
-    f32x4 tmp[NIT];
+  // the six B^T d rows of task (ty, col, c4) from its six input rows d (w4_bt over rows)
+  auto bt_store = [&](int ty, int col, int c4, const f32x4 (&d)[6]) {
+    f32x4 bt[6];
+    w4_bt(d, bt);
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-      const int e = i * NTH + tid;
-      const int c4 = e & 15, p = e >> 4, row = p / LCOL, col = p - (p / LCOL) * LCOL;
-      tmp[i] = e < NSTAGE ? load_in(row - 1, col - 1, c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 6; ++r) *reinterpret_cast<f32x4*>(&smem[tpix(6 * ty + r, col) + c4 * 4]) = bt[r];
+  };
+  // ---- stage the first layer's B^T d rows straight from its input (zero outside the image) ----
+  {
+    f32x4 tmp[NBT][6];
+#pragma unroll
+    for (int k = 0; k < NBT; ++k) {
+      int ty, col, c4;
+      bt_task(tid, k, ty, col, c4);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) tmp[k][r] = load_in(4 * ty + r - 1, col - 1, c4);
     }
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-      const int e = i * NTH + tid;
-      const int c4 = e & 15, p = e >> 4, row = p / LCOL, col = p - (p / LCOL) * LCOL;
-      if (e < NSTAGE) *reinterpret_cast<f32x4*>(&smem[tpix(row, col) + c4 * 4]) = tmp[i];
+    for (int k = 0; k < NBT; ++k) {
+      int ty, col, c4;
+      bt_task(tid, k, ty, col, c4);
+      bt_store(ty, col, c4, tmp[k]);
     }
   }
 
@@ -160,28 +178,11 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
   __syncthreads();
   stamp(1);
 
-  // ---- row xi of B^T d for tile li (conv3x3_wino4_kernel's exact operations) ----
+  // ---- row xi of B^T d for tile li, column j, chunk kc: one staged value ----
   const int ty = li / TTX, tx = li % TTX;
-  const int tbase = (4 * ty) * RS + tx * PS + lg * 4;
-  const int re = xi == 5 ? 5 : 0;
-  const float c1 = kW4BT[xi][1], c2 = kW4BT[xi][2], c3 = kW4BT[xi][3], c4c = kW4BT[xi][4];
-  const float ce = (xi == 0 || xi == 5) ? 1.f : 0.f;
-  auto ld = [&](int i, int j, int kc) -> f32x4 {
-    return *reinterpret_cast<const f32x4*>(&smem[tbase + i * RS + ((j & 3) * HPP + (j >> 2)) * PS + kc * 16]);
-  };
-  auto ldcol = [&](int j, int kc, f32x4 (&d)[5]) {
-    d[0] = ld(1, j, kc);
-    d[1] = ld(2, j, kc);
-    d[2] = ld(3, j, kc);
-    d[3] = ld(4, j, kc);
-    d[4] = ld(re, j, kc);
-  };
-  auto rcol = [&](const f32x4 (&d)[5]) {
-    f32x4 s = c1 * d[0];
-    s = fma4s(c2, d[1], s);
-    s = fma4s(c3, d[2], s);
-    s = fma4s(c4c, d[3], s);
-    return fma4s(ce, d[4], s);
+  const int tbase = (6 * ty + xi) * RS + tx * PS + lg * 4;
+  auto ld = [&](int j, int kc) -> f32x4 {
+    return *reinterpret_cast<const f32x4*>(&smem[tbase + ((j & 3) * HPP + (j >> 2)) * PS + kc * 16]);
   };
 
   bool failed = false;
@@ -195,12 +196,9 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
     // (t, nu) order; the next chunk's columns are read before and combined after each group
     f32x4 V[6];
     {
-      f32x4 r[6], d[5];
+      f32x4 r[6];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        ldcol(j, 0, d);
-        r[j] = rcol(d);
-      }
+      for (int j = 0; j < 6; ++j) r[j] = ld(j, 0);
       w4_bt(r, V);
     }
     f32x4 acc[6];
@@ -211,10 +209,10 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
       const bool next = kc + 1 < KC;
       if (next) wload(wl, kc + 1, av[(kc + 1) & 1]);
       else if (!last) wload(wsrc(l + 1), 0, av[0]);  // the next layer's first chunk
-      f32x4 rn[6], dn[5];
+      f32x4 rn[6];
 #pragma unroll
       for (int g = 0; g < 6; ++g) {
-        if (next) ldcol(g, kc + 1, dn);
+        if (next) rn[g] = ld(g, kc + 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 4 * g; m < 4 * g + 4; ++m) {
@@ -222,7 +220,6 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
           acc[nu] = mfma4(av[kc & 1][nu][tt], V[nu][tt], acc[nu]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (next) rn[g] = rcol(dn);
       }
       if (next) w4_bt(rn, V);
     }
@@ -314,10 +311,12 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
         if (keep) resid[ay] = y[ay];
       }
     }
-    // the zero ring pixels the exchange overwrote: row 0, and columns 0 / 17 of rows 1..5
-    for (int e = tl; e < 28 * 16; e += NTH) {
+    // the zero ring of the raw 18x18 input (the B^T d rows and the exchange overwrote it):
+    // rows 0 / 17, and columns 0 / 17 of rows 1..16
+    for (int e = tl; e < 68 * 16; e += NTH) {
       const int rp = e >> 4, c4 = e & 15;
-      const int row = rp < 18 ? 0 : 1 + ((rp - 18) >> 1), col = rp < 18 ? rp : (((rp - 18) & 1) ? 17 : 0);
+      const int row = rp < 36 ? (rp < 18 ? 0 : 17) : 1 + ((rp - 36) >> 1);
+      const int col = rp < 36 ? (rp < 18 ? rp : rp - 18) : (((rp - 36) & 1) ? 17 : 0);
       *reinterpret_cast<f32x4*>(&smem[tpix(row, col) + 4 * c4]) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -355,6 +354,25 @@ __global__ void __launch_bounds__(pchain::NTH) wino4_pchain_kernel(const ChainAr
         const int e = k * NTH + tl, p = e >> 10, qp = p < q ? p : p + 1, f = e & 1023;
         const int px = f >> 2, c4 = f & 3;
         *reinterpret_cast<f32x4*>(&smem[tpix((px >> 4) + 1, (px & 15) + 1) + CQ * qp + 4 * c4]) = hv[k];
+      }
+    }
+    __syncthreads();
+    // ---- the next layer's B^T d rows from the raw tile (read all, then overwrite) ----
+    {
+      f32x4 d[NBT][6];
+#pragma unroll
+      for (int k = 0; k < NBT; ++k) {
+        int ty2, col, c4;
+        bt_task(tl, k, ty2, col, c4);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) d[k][r] = *reinterpret_cast<const f32x4*>(&smem[tpix(4 * ty2 + r, col) + c4 * 4]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < NBT; ++k) {
+        int ty2, col, c4;
+        bt_task(tl, k, ty2, col, c4);
+        bt_store(ty2, col, c4, d[k]);
       }
     }
     __syncthreads();
