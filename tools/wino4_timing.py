@@ -27,7 +27,10 @@ def main():
     ap.add_argument("--res", type=int, default=1)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--probe", type=int, default=0, help="TIC_WINO4_PROBE bits (results invalid)")
+    ap.add_argument("--tile", default=None, help='TIC_FORCE_TILE, e.g. "4,1,5,1,4" (th, 1, 5, 1, tiles per workgroup)')
     args = ap.parse_args()
+    if args.tile:
+        os.environ["TIC_FORCE_TILE"] = args.tile
     sys.path.insert(0, ROOT)
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
