@@ -1,6 +1,6 @@
-# round 4 evidence on the current sources (shipped tuning): PMC traffic per lane batch, the
+# evidence on the current sources (shipped tuning): PMC traffic per lane batch, the
 # driver-protocol bench line and the 200-step one for configs[1], configs[2], configs[4],
-# configs[3] (world 1), rocprofv3 kernel stats of the default bench.   bash tools/gpu_r04_evidence.sh <tag>
+# configs[3] (world 1), rocprofv3 kernel stats of the default bench.   bash tools/gpu_evidence.sh <tag>
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r04}
 cd $R
