@@ -202,6 +202,9 @@ def test_chain_shortened_where_a_long_run_cannot_be_resident():
     with Codec(0, synthetic_params(0), SYNTH_MEAN, SYNTH_STD, patch_size=P, tuning="none") as c:
         c.set_option("s1_form", 1)
         c.set_option("chain", 1)
+        # at most 8 patches per launch: the default chunk (256) of 4096x4096 patches would put
+        # the hand-off buffer's byte offsets past 2^31 and decline every chain (the other guard)
+        c.set_option("chunk", 8)
         kern = c.layer_kernels(1)
         starts = [i for i, k in enumerate(kern) if k.startswith("wino_chain_kernel")]
         assert starts, kern

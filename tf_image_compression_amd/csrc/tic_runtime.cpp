@@ -753,7 +753,9 @@ static int chain_end(const tic_handle* h, int li) {
     const int per_region = h->chain_wh >= 3 ? 2 : 1;  // workgroups per region
     const long slots = (long)h->num_cus * (h->chain_wh == 2 || h->chain_wh == 4 ? 1 : 2);
     auto need = [&](int nl) { return 2L * h->nlanes * per_region * std::min(R, (long)(nl - 1) * (rw + 1) + 1); };
-    while (j - li >= 2 && need(j - li) > slots) --j;
+    // (a shortened run never ends inside a res_block: the chain keeps a block input it read in
+    // LDS only, so the block's residual conv must run inside the same launch)
+    while (j - li >= 2 && (need(j - li) > slots || h->layers[j].def.residual)) --j;
     if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
   }
   // (form 2: four workgroups of a patch wait for each other; one per CU is always resident)
@@ -1025,6 +1027,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.in = first_dec ? in : (const void*)src;
       a.wp = lay.d_w;
       a.bias = lay.d_b;
+      if (d.residual && block_in < 0)  // (a chain run ending inside a res_block: never planned)
+        return fail(TIC_EINVAL, "layer %s: residual input not in a workspace", d.name.c_str());
       a.res = d.residual ? ws[block_in] : nullptr;
       a.out = last_enc ? d_pre : ws[dst];
       a.qout = last_enc ? d_idx : nullptr;
