@@ -857,15 +857,35 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
     constexpr int NBL = 2 * LR1 + (LR1 + 15) / 16;
     constexpr int NPW = (NBL + 3) / 4;  // blocks per wave
     f32x4 res[CMP ? NPW : 1][NB0];       // CMP: layer-0 results held until the RGB planes are dead
-    auto put0 = [&](int slot, bool valid, const f32x4 (&acc)[NB0]) {
+    // + bias (two packed adds), ReLU, zero outside layer 0's image, into the layer-1 tile at
+    // float offset off(nb) — the same operations as conv3x3_kernel's epilogue
+    auto put0v = [&](bool valid, const f32x4 (&acc)[NB0], auto&& off) {
 #pragma unroll
       for (int nb = 0; nb < NB0; ++nb) {
-        f32x4 v = acc[nb];
-        v.x = valid ? fmaxf(__fadd_rn(v.x, bb[nb].x), 0.f) : 0.f;
-        v.y = valid ? fmaxf(__fadd_rn(v.y, bb[nb].y), 0.f) : 0.f;
-        v.z = valid ? fmaxf(__fadd_rn(v.z, bb[nb].z), 0.f) : 0.f;
-        v.w = valid ? fmaxf(__fadd_rn(v.w, bb[nb].w), 0.f) : 0.f;
-        *reinterpret_cast<f32x4*>(&t1[t1c(slot, nb * 4 + lg)]) = v;
+        f32x4 v = acc[nb] + bb[nb];
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+        if (!valid) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(&t1[off(nb)]) = v;
+      }
+    };
+    auto put0 = [&](int slot, bool valid, const f32x4 (&acc)[NB0]) {
+      put0v(valid, acc, [&](int nb) { return t1c(slot, nb * 4 + lg); });
+    };
+    // a main block jb of this wave (blk = wave + 4 jb < 2 LR1): slot s0 + 2 LC1 jb, its swizzle
+    // key (k0 + 2 LC1 jb / GRP) mod NCH — the per-lane parts computed once
+    const int s0 = (wave >> 1) * LC1 + (wave & 1) * 17 + li;
+    const int k0 = (s0 / GRP) % NCH;
+    static_assert((2 * LC1) % GRP == 0 && (NCH & (NCH - 1)) == 0, "main-block slot stride");
+    auto put0_main = [&](int jb, bool valid, const f32x4 (&acc)[NB0]) {
+      const int slot = s0 + 2 * LC1 * jb;
+      if constexpr (CMP) {
+        const int key = (k0 + (2 * LC1 / GRP) * jb) & (NCH - 1);
+        put0v(valid, acc, [&](int nb) { return slot * PS1 + 4 * ((nb * 4 + lg) ^ key); });
+      } else {
+        put0v(valid, acc, [&](int nb) { return slot * PS1 + 4 * (nb * 4 + lg); });
       }
     };
     // lane li's slot in block blk, whether the block holds it, and whether it lies inside
@@ -892,12 +912,16 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
       dw[t] = d < 0 ? 0 : d;
       dz[t] = dl[0][t] < 0 ? 0 : dl[0][t];
     }
+    // main blocks: row (blk >> 1) = (wave >> 1) + 2 jb, so the per-lane part of the 7 offsets is
+    // fixed and block jb adds a constant (the read's immediate offset)
+    const float* gw[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) gw[t] = rgb + (wave >> 1) * 8 * QJ + li + dw[t];
     auto gather = [&](int jb, float (&b)[7]) {
       const int blk = wave + 4 * jb;
       if (blk < 2 * LR1) {  // wave-uniform
-        const int base = (blk >> 1) * 8 * QJ + li;
 #pragma unroll
-        for (int t = 0; t < 7; ++t) b[t] = rgb[base + dw[t]];
+        for (int t = 0; t < 7; ++t) b[t] = gw[t][jb * 16 * QJ];
       } else {
         const int base = (lo_row(blk) < LR1 ? lo_row(blk) : 0) * 8 * QJ + 16;
 #pragma unroll
@@ -927,6 +951,8 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
       if constexpr (CMP) {
 #pragma unroll
         for (int nb = 0; nb < NB0; ++nb) res[jb][nb] = acc[nb];
+      } else if (blk < 2 * LR1) {
+        put0_main(jb, inner0 || blk_valid(blk), acc);
       } else if (blk_has(blk)) {
         put0(blk_slot(blk), blk_valid(blk), acc);
       }
@@ -936,7 +962,8 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
 #pragma unroll
       for (int jb = 0; jb < NPW; ++jb) {
         const int blk = wave + 4 * jb;
-        if (blk < NBL && blk_has(blk)) put0(blk_slot(blk), blk_valid(blk), res[jb]);
+        if (blk < 2 * LR1) put0_main(jb, inner0 || blk_valid(blk), res[jb]);
+        else if (blk < NBL && blk_has(blk)) put0(blk_slot(blk), blk_valid(blk), res[jb]);
       }
     }
   }
