@@ -753,11 +753,13 @@ static int chain_end(const tic_handle* h, int li) {
     const int per_region = h->chain_wh >= 3 ? 2 : 1;  // workgroups per region
     const long slots = (long)h->num_cus * (h->chain_wh == 2 || h->chain_wh == 4 ? 1 : 2);
     auto need = [&](int nl) { return 2L * h->nlanes * per_region * std::min(R, (long)(nl - 1) * (rw + 1) + 1); };
-    // (a shortened run never ends inside a res_block: the chain keeps a block input it read in
-    // LDS only, so the block's residual conv must run inside the same launch)
-    while (j - li >= 2 && (need(j - li) > slots || h->layers[j].def.residual)) --j;
+    while (j - li >= 2 && need(j - li) > slots) --j;
     if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
   }
+  // A run cut short (residency above, or CH_MAX_LAYERS) never ends inside a res_block: the
+  // chain keeps a block input it read in LDS only, so the block's residual conv must run in
+  // the same launch (after a run, the per-layer path has no block input in a workspace)
+  while (j - li >= 2 && h->layers[j].def.residual) --j;
   // (form 2: four workgroups of a patch wait for each other; one per CU is always resident)
   return j - li >= 2 ? j : li;
 }
