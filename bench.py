@@ -645,10 +645,11 @@ def tune_cache_path(args, M, P, B):
     return args.tune_cache, save or args.tune_cache
 
 
-def tune(args, codec, d_in, B, lane_b, M, P):
+def tune(args, codec, d_in, B, lane_b, M, P, search=True):
     """Per-layer autotune + in-situ step tuning (outside the timed region), or the replay of
     the shipped tuning state (tf_image_compression_amd/tune/, the same file Codec applies by
-    default) when it was measured on these kernel sources and this configuration."""
+    default) when it was measured on these kernel sources and this configuration.  With
+    search False only the replay is done (the runtime's defaults stand without one)."""
     from tf_image_compression_amd import tuning
     path, save = tune_cache_path(args, M, P, B)
     stamp = tuning.stamp(M, P, B, args.streams, args.tune_step)
@@ -657,6 +658,8 @@ def tune(args, codec, d_in, B, lane_b, M, P):
         if doc.get("_meta") == stamp:
             codec.tuning_import(doc["tuning"])
             return os.path.relpath(path, ROOT)
+    if not search:
+        return "none (no replayable tuning; a shard smaller than one batch on some rank)"
     codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice
     if args.tune_step > 0:  # then per layer by the whole step as it runs (both lanes)
         codec.autotune_step(d_in, B, rounds=args.tune_step, reps=5)
@@ -719,8 +722,11 @@ def main_sharded(args):
     t_gen = time.perf_counter() - t_gen
     lane_b = -(-B // max(1, min(args.streams, B)))
     tuning = "none"
-    if not args.no_autotune and shard.n >= B:
-        tuning = tune(args, codec, shard.d_img, B, lane_b, M, P)
+    # the same decision on every rank: searching needs a full batch on the
+    # rank's own shard, so it runs everywhere or nowhere; the replay needs no shard
+    search = dist.all_ranks(comm, shard.n >= B)
+    if not args.no_autotune:
+        tuning = tune(args, codec, shard.d_img, B, lane_b, M, P, search=search)
     for _ in range(args.warmup):
         shard.enqueue()
     codec.synchronize()

@@ -18,7 +18,16 @@ from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH
 def main():
     out, n_images, P = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
     driver = sys.argv[4] if len(sys.argv) > 4 else "host"
-    comm = dist.GlooComm()
+    comm = dist.make_comm()  # gloo at world > 1; one barrier under the init bound
+    if driver == "late":  # rank 1 arrives at the next collective late (tuning on one rank)
+        import time
+        if comm.rank == 1:
+            time.sleep(float(os.environ.get("LATE_S", "3")))
+        ok = dist.all_ranks(comm, comm.rank == 0)
+        with open(f"{out}.{comm.rank}", "w") as f:
+            json.dump({"rank": comm.rank, "all_ranks": ok, "all_true": dist.all_ranks(comm, True)}, f)
+        comm.close()
+        return
     params = synthetic_params(1)
 
     if driver == "device":  # the GPU driver's orchestration (sharded.run_device_shard)

@@ -121,12 +121,45 @@ def test_deadline_ends_a_stalled_wait():
     missing peer fails fast instead of hanging."""
     code = ("import time\nfrom tf_image_compression_amd import dist\n"
             "with dist.Deadline('ncclCommInitRank (world 8)', 0.5, rank=5):\n    time.sleep(30)\n")
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60,
-                       env=dict(os.environ, PYTHONPATH=ROOT))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TIC_DIST_")}  # (ADVICE r04)
+    env["PYTHONPATH"] = ROOT
+    env["TIC_DIST_TIMEOUT"] = "600"  # an explicit bound wins over the init-bound override
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 3
     assert "[rank 5] ncclCommInitRank (world 8) did not complete within 0 s" in r.stderr or \
         "[rank 5] ncclCommInitRank (world 8) did not complete within 1 s" in r.stderr
     ok = subprocess.run([sys.executable, "-c", "from tf_image_compression_amd import dist\n"
                          "with dist.Deadline('x', 5.0, rank=0):\n    pass\nprint('done')"],
-                        cwd=ROOT, capture_output=True, text=True, timeout=60, env=dict(os.environ, PYTHONPATH=ROOT))
+                        cwd=ROOT, capture_output=True, text=True, timeout=60, env=env)
     assert ok.returncode == 0 and ok.stdout.strip() == "done"
+
+
+def _run_late(tmp_path, env_extra):
+    port = _free_port()
+    out = str(tmp_path / "late")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TIC_DIST_")}
+    env.update(PYTHONPATH=ROOT, OMP_NUM_THREADS="1", LATE_S="4", **env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "dist_worker.py"),
+           out, "0", "0", "late"]
+    r = subprocess.run(cmd, env=env, timeout=120, cwd=ROOT, capture_output=True, text=True)
+    return r, out
+
+
+def test_late_peer_within_collective_bound(tmp_path):
+    """a collective also waits for its peers to arrive, and a peer may arrive late
+    after rank-dependent work (tuning on one rank).  Rank 1 reaches its first collective 4 s
+    after the start-up barrier; with a 2 s init bound that run must still pass (collectives
+    have their own, longer bound), and dist.all_ranks gives every rank the same decision."""
+    r, out = _run_late(tmp_path, {"TIC_DIST_TIMEOUT": "2"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = [json.load(open(f"{out}.{k}")) for k in range(2)]
+    assert [x["all_ranks"] for x in res] == [False, False] and all(x["all_true"] for x in res)
+
+
+def test_late_peer_beyond_collective_bound(tmp_path):
+    """The same late arrival with the collective bound set under it: rank 0 ends with exit
+    code 3 and names the wait instead of hanging."""
+    r, _ = _run_late(tmp_path, {"TIC_DIST_COLLECTIVE_TIMEOUT": "1"})
+    assert r.returncode != 0
+    assert "gloo all_reduce(max) did not complete within 1 s" in r.stderr

@@ -85,16 +85,34 @@ def env_rank() -> tuple[int, int, int]:
     return rank, world, local
 
 
+# Bounds of the blocking waits (seconds).  Creating the communicator and the id rendezvous
+# happen right after every rank starts, so a short bound catches a missing peer early
+# (TIC_DIST_TIMEOUT).  A collective also waits for every peer to ARRIVE at it, and peers
+# arrive after rank-dependent work (tuning, measurement, an uneven shard), so collectives
+# get a bound sized for that work, not for the collective itself (TIC_DIST_COLLECTIVE_TIMEOUT).
+INIT_TIMEOUT = 150.0
+COLLECTIVE_TIMEOUT = 1800.0
+
+
+def init_timeout() -> float:
+    return float(os.environ.get("TIC_DIST_TIMEOUT", INIT_TIMEOUT))
+
+
+def collective_timeout() -> float:
+    return float(os.environ.get("TIC_DIST_COLLECTIVE_TIMEOUT", COLLECTIVE_TIMEOUT))
+
+
 class Deadline:
     """A bounded wait around a blocking call that can hang when a peer never arrives (RCCL
     communicator creation, a collective and its synchronisation, the id rendezvous): if the
     call has not returned after `seconds`, say which rank waited for what and end the process
     with exit code 3 — a clear failure instead of a stalled multi-GPU run (never a re-exec;
-    the GPU is released by the process exit).  TIC_DIST_TIMEOUT overrides the default."""
+    the GPU is released by the process exit).  An explicit `seconds` is used as given; with
+    None the init bound applies (init_timeout(): TIC_DIST_TIMEOUT or 150 s)."""
 
     def __init__(self, what: str, seconds: float | None = None, rank: int | None = None):
         self.what = what
-        self.seconds = float(os.environ.get("TIC_DIST_TIMEOUT", seconds if seconds is not None else 120.0))
+        self.seconds = float(seconds) if seconds is not None else init_timeout()
         self.rank = env_rank()[0] if rank is None else rank
         self._timer = None
 
@@ -118,16 +136,16 @@ class Deadline:
 class LocalComm:
     rank, world = 0, 1
 
-    def barrier(self):
+    def barrier(self, timeout: float | None = None):
         pass
 
-    def allreduce_max(self, x: float) -> float:
+    def allreduce_max(self, x: float, timeout: float | None = None) -> float:
         return float(x)
 
     def allgather_stats(self, s: RankStats) -> list[RankStats]:
         return [s]
 
-    def allgather_f64(self, a) -> np.ndarray:
+    def allgather_f64(self, a, timeout: float | None = None) -> np.ndarray:
         return np.asarray(a, np.float64).reshape(1, -1)
 
     def close(self):
@@ -135,36 +153,40 @@ class LocalComm:
 
 
 class GlooComm:
-    """torch.distributed (gloo, CPU) — for CPU tests of the multi-rank path only."""
+    """torch.distributed (gloo, CPU) — for CPU tests of the multi-rank path only; its waits
+    carry the same bounds as RcclComm's."""
 
     def __init__(self):
         import torch.distributed as dist  # imported lazily: never in GPU processes
         self.dist = dist
         if not dist.is_initialized():
-            dist.init_process_group("gloo")
+            with Deadline("gloo init_process_group", init_timeout()):
+                dist.init_process_group("gloo")
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
 
-    def barrier(self):
-        self.dist.barrier()
+    def _bound(self, what, timeout):
+        return Deadline(what, collective_timeout() if timeout is None else timeout, self.rank)
 
-    def allreduce_max(self, x: float) -> float:
+    def barrier(self, timeout: float | None = None):
+        with self._bound("gloo barrier", timeout):
+            self.dist.barrier()
+
+    def allreduce_max(self, x: float, timeout: float | None = None) -> float:
         import torch
         t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        with self._bound("gloo all_reduce(max)", timeout):
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def allgather_stats(self, s: RankStats) -> list[RankStats]:
-        import torch
-        t = torch.from_numpy(s.to_array())
-        out = [torch.zeros(6, dtype=torch.float64) for _ in range(self.world)]
-        self.dist.all_gather(out, t)
-        return [RankStats.from_array(o.numpy()) for o in out]
+        return [RankStats.from_array(r) for r in self.allgather_f64(s.to_array())]
 
-    def allgather_f64(self, a) -> np.ndarray:
+    def allgather_f64(self, a, timeout: float | None = None) -> np.ndarray:
         import torch
         t = torch.from_numpy(np.ascontiguousarray(a, np.float64).reshape(-1))
         out = [torch.zeros_like(t) for _ in range(self.world)]
-        self.dist.all_gather(out, t)
+        with self._bound("gloo all_gather", timeout):
+            self.dist.all_gather(out, t)
         return np.stack([o.numpy() for o in out])
 
     def close(self):
@@ -255,11 +277,11 @@ class RcclComm:
             self._ok(self.nccl.ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = port or int(os.environ.get("TIC_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 17))
-        with Deadline(f"ncclUniqueId rendezvous on {addr}:{port}", 150.0, rank):
+        with Deadline(f"ncclUniqueId rendezvous on {addr}:{port}", init_timeout(), rank):
             raw = exchange_unique_id(rank, world, uid_to_bytes(uid) if rank == 0 else None, addr, port)
         uid = uid_from_bytes(raw)
         self.comm = C.c_void_p()
-        with Deadline(f"ncclCommInitRank (world {world})", 120.0, rank):
+        with Deadline(f"ncclCommInitRank (world {world})", init_timeout(), rank):
             self._ok(self.nccl.ncclCommInitRank(C.byref(self.comm), world, uid, rank), "ncclCommInitRank")
         self.stream = codec.stream_ptr()
         # every collective below is followed by a synchronisation, so nothing of ours stays
@@ -273,24 +295,24 @@ class RcclComm:
         if rc != 0:
             raise RuntimeError(f"{what}: {self.nccl.ncclGetErrorString(rc).decode()} ({rc})")
 
-    def allreduce_max(self, x: float) -> float:
+    def allreduce_max(self, x: float, timeout: float | None = None) -> float:
         self.d_send.upload(np.array([x], np.float64))
-        with Deadline("ncclAllReduce(max)", 60.0, self.rank):
+        with Deadline("ncclAllReduce(max)", collective_timeout() if timeout is None else timeout, self.rank):
             self._ok(self.nccl.ncclAllReduce(self.d_send.ptr, self.d_recv.ptr, 1, NCCL_FLOAT64, NCCL_MAX, self.comm,
                                              self.stream), "ncclAllReduce")
             self.codec.synchronize()
         return float(self.d_recv.download((1,), np.float64)[0])
 
-    def barrier(self):
-        self.allreduce_max(0.0)
+    def barrier(self, timeout: float | None = None):
+        self.allreduce_max(0.0, timeout)
 
-    def allgather_f64(self, a) -> np.ndarray:
+    def allgather_f64(self, a, timeout: float | None = None) -> np.ndarray:
         """[world, k] f64: every rank's k words (k <= 16), one ncclAllGather on the codec stream."""
         a = np.ascontiguousarray(a, np.float64).reshape(-1)
         if a.size > self.cap:
             raise ValueError(f"allgather_f64 carries at most {self.cap} words per rank")
         self.d_send.upload(a)
-        with Deadline("ncclAllGather", 60.0, self.rank):
+        with Deadline("ncclAllGather", collective_timeout() if timeout is None else timeout, self.rank):
             self._ok(self.nccl.ncclAllGather(self.d_send.ptr, self.d_recv.ptr, a.size, NCCL_FLOAT64, self.comm,
                                              self.stream), "ncclAllGather")
             self.codec.synchronize()
@@ -306,10 +328,20 @@ class RcclComm:
 
 
 def make_comm(codec=None):
-    """LocalComm at world size 1, RcclComm on a GPU codec otherwise."""
+    """LocalComm at world size 1, RcclComm on a GPU codec otherwise.  Every rank passes one
+    barrier here, under the short init bound, before any rank-dependent work: a missing peer
+    is reported at start-up, and the later collectives only wait for work, never for a rank
+    that is not there."""
     rank, world, _ = env_rank()
     if world == 1:
         return LocalComm()
-    if codec is None:
-        return GlooComm()
-    return RcclComm(codec, rank, world)
+    comm = GlooComm() if codec is None else RcclComm(codec, rank, world)
+    comm.barrier(init_timeout())
+    return comm
+
+
+def all_ranks(comm, flag: bool) -> bool:
+    """True on every rank iff `flag` is true on every rank (one max-reduce of the negation):
+    a decision every rank must take alike (e.g. whether to run the minutes-long tuning
+    before the first barrier) is taken from all ranks' inputs."""
+    return comm.allreduce_max(0.0 if flag else 1.0) == 0.0
