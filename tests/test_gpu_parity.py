@@ -38,10 +38,7 @@ def lib_codec():
         c.close()
 
 
-TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1), (2, 2), (4, 4), (1, 1)] for wl in (0, 1, 2, 3)]
-
-# (cin, cout) of the persistent, weights-in-LDS variants (conv_s2.hip / conv_t2.hip)
-PERSIST = {K_S2: {(16, 32), (32, 32), (32, 64)}, K_T2: {(32, 32), (32, 16), (64, 32)}}
+TILES = [(th, ns, wl) for th, ns in [(4, 1), (4, 2), (8, 1), (2, 1), (2, 2), (4, 4), (1, 1)] for wl in (0, 1, 2)]
 
 LAYER_CASES = [
     (K_S1, 64, 64, 1, False, 16, 16),
@@ -90,25 +87,18 @@ def test_conv3x3_layer(lib_codec, kind, cin, cout, act, res, H, W):
     try:
         for th, ns, wl in TILES:
             os.environ["TIC_FORCE_TILE"] = f"{th},{ns},{wl}"
-            # persistent variants (wl 3): also with a grid of 3 workgroups, so each walks
-            # several tiles through its double-buffered input
-            for cap in ((0, 3) if wl == 3 else (0,)):
-                codec.set_option("persist_grid", cap)
-                try:
-                    codec.conv3x3_device(kind, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
-                except TicError as e:
-                    assert "no compiled" in str(e)
-                    break
-                outs.append(((th, ns, wl, cap), d_out.download(ref.shape, np.float32)))
+            try:
+                codec.conv3x3_device(kind, act, d_in, n, H, W, cin, cout, k, b, d_res, d_out)
+            except TicError as e:
+                assert "no compiled" in str(e)
+                continue
+            outs.append(((th, ns, wl), d_out.download(ref.shape, np.float32)))
     finally:
         os.environ.pop("TIC_FORCE_TILE", None)
-        codec.set_option("persist_grid", 0)
     for buf in (d_in, d_out, d_res):
         if buf is not None:
             buf.free()
     assert outs, "no compiled tiling for this layer"
-    if kind != K_S1 and act == 1 and not res and (cin, cout) in PERSIST[kind]:
-        assert any(t[2] == 3 for t, _ in outs), "persistent variant did not run"
     scale = max(1.0, float(np.max(np.abs(ref))))
     for tile, got in outs:
         err = float(np.max(np.abs(got - ref)))

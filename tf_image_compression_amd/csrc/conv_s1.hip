@@ -64,8 +64,7 @@ static const ConvEntry kS1[] = {
     S1_128(64, 128, ACT_ID, false, IN_IDX, OUT_F32),
     S1_WINO4(ACT_RELU, false, IN_F32, OUT_F32),
     S1_WINO4(ACT_RELU, true, IN_F32, OUT_F32),
-    // model_0/1 encode_4 (quantiser) and decode_4 (dequantiser) in F(4x4,3x3): the form the
-    // 16x16 patch chain (wino4_pchain.h) reproduces for every layer of its runs
+    // model_0/1 encode_4 (quantiser) and decode_4 (dequantiser) in F(4x4,3x3) (s1_form 2)
     S1_WINO4(ACT_ID, false, IN_F32, OUT_QUANT),
     S1_WINO4(ACT_ID, false, IN_IDX, OUT_F32),
 };

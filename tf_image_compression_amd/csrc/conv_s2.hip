@@ -24,10 +24,6 @@ static const ConvEntry kS2[] = {
     // base_model/ch_128 encode_2 (64 -> 128)
     TIC_CONVL2(MODE_S2, 64, 128, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONVL2(MODE_S2, 64, 128, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PERSIST(MODE_S2, 16, 32, 4, 4, ACT_RELU),
-    TIC_PERSIST(MODE_S2, 32, 32, 4, 4, ACT_RELU),
-    TIC_PERSIST(MODE_S2, 32, 32, 2, 2, ACT_RELU),
-    TIC_PERSIST(MODE_S2, 32, 64, 2, 2, ACT_RELU),
 };
 const ConvEntry* conv_registry_s2(int* count) {
   *count = sizeof(kS2) / sizeof(kS2[0]);

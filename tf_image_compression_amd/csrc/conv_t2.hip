@@ -26,11 +26,6 @@ static const ConvEntry kT2[] = {
     TIC_CONVL2(MODE_T2, 128, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONVL2(MODE_T2, 128, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONVL2(MODE_T2, 128, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_PERSIST(MODE_T2, 32, 32, 4, 4, ACT_RELU),
-    TIC_PERSIST(MODE_T2, 32, 32, 8, 4, ACT_RELU),
-    TIC_PERSIST(MODE_T2, 32, 16, 4, 4, ACT_RELU),
-    TIC_PERSIST(MODE_T2, 32, 16, 8, 4, ACT_RELU),
-    TIC_PERSIST(MODE_T2, 64, 32, 4, 4, ACT_RELU),
 };
 const ConvEntry* conv_registry_t2(int* count) {
   *count = sizeof(kT2) / sizeof(kT2[0]);

@@ -95,7 +95,6 @@ struct ConvEntry {
   int wr;             // wave row-groups
   int nsplit;         // workgroups splitting the output channels of one pixel tile
   int wlds;           // weight source: 0 L2 (prefetch 2), 1 LDS-DMA ring, 2 L2 (prefetch 6),
-                      // 3 all weights resident in LDS, persistent workgroups (conv3x3_persist.h)
   ConvLaunch fn;
 };
 
@@ -126,13 +125,8 @@ bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int 
 // wino_chain.h; false if the mode combination is not compiled.
 struct ChainArgs;
 // wh: 1 = 256-thread workgroups, 2 = 512-thread workgroups (output channels split in halves
-// over the waves), 3 / 4 = two 256- / 512-thread workgroups per region (output channels split
-// in halves over the workgroups: wino_chain_cs.h)
+// over the waves)
 bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh);
-// A chain of stride-1 64->64 layers on a map of at most 16x16 in Winograd F(4x4,3x3), four
-// workgroups per patch (one per quarter of the output channels; wino4_pchain.h); false if
-// the geometry or the mode combination is not supported.
-bool launch_wino4_pchain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s);
 
 // Whole-image glue and the symbol histogram (image_ops.hip).
 void launch_tile_reflect(const uint8_t* img, int H, int W, int P, int hn, int wn, uint8_t* out, int num_cus,

@@ -183,7 +183,6 @@ bool wino4_fits(const tic::ConvEntry& c, int hg, int wg) {
 
 bool form_match(const tic::ConvEntry& c, int form, int fwl) {
   if (fwl >= 0) return c.wlds == fwl;
-  if (c.wlds == 3) return false;  // persistent variants: only by autotune or forced
   return entry_form(c) == form;
 }
 
@@ -252,7 +251,7 @@ std::vector<const tic::ConvEntry*> conv_candidates(int mode, int cin, int cout, 
     if (fm < 0) break;
     for (int i = 0; i < cnt; ++i)
       if (e[i].cin == cin && e[i].cout == cout && e[i].act == act && e[i].res == res && e[i].in == in &&
-          e[i].out == outm && e[i].wlds != 3 && entry_form(e[i]) == fm && wino4_fits(e[i], hg, wg))
+          e[i].out == outm && entry_form(e[i]) == fm && wino4_fits(e[i], hg, wg))
         out.push_back(&e[i]);
   }
   return out;
@@ -533,10 +532,10 @@ int ensure_ws(tic_handle* h, Lane& ln, int n) {
 // Grow a lane's chain hand-off buffers for a chain of nl layers over n patches of R
 // regions.  Fresh flags are zero, below every launch's epoch + 1, so nothing else is reset.
 int ensure_chain(tic_handle* h, Lane& ln, int nl, int n, int R) {
-  // sized for the channel-split shape (two 8 KB half-interiors and two flags per region),
-  // which covers the others (one 8 KB border record and one flag per region)
+  // one 8 KB border record (4 sides x 8 pixels x 64 channels) and one flag per region and
+  // hand-off
   const size_t nR = (size_t)n * R;
-  const size_t xf = (size_t)(nl - 1) * nR * 2 * 64 * 32, nf = (size_t)(nl - 1) * nR * 2;
+  const size_t xf = (size_t)(nl - 1) * nR * 4 * 8 * 64, nf = (size_t)(nl - 1) * nR;
   if (!ln.ctl) {
     HIP_TRY(hipMalloc((void**)&ln.ctl, 4 * sizeof(unsigned)));
     HIP_TRY(hipMemsetAsync(ln.ctl, 0, 4 * sizeof(unsigned), ln.stream));
@@ -723,15 +722,12 @@ static bool fuses_tail(const tic_handle* h) {
 // li starts a run of >= 2 stride-1 64->64 layers inside one network half (the encoder's last
 // layer may end a run with the quantiser, the decoder's first may start one with the
 // dequantiser), and the stride-1 form has a chain kernel that reproduces it bit for bit:
-// F(2x2,3x3) (form 1) -> wino_chain_kernel / wino_chain_cs_kernel (8x8 regions handing
-// borders to their neighbours); F(4x4,3x3) (form 2) on maps of at most 16x16 ->
-// wino4_pchain_kernel (four channel-quarter workgroups per patch, no spatial hand-off).
-// Returns li when no chain starts there.
-static bool pchain_form(const tic_handle* h, int li) { return h->s1_form == 2 && h->layers[li].h_in <= 16; }
+// F(2x2,3x3) (form 1) -> wino_chain_kernel (8x8 regions handing borders to their
+// neighbours).  Returns li when no chain starts there.
 static int chain_end(const tic_handle* h, int li) {
   const int L = (int)h->layers.size();
   if (!h->chain || li == 0 || li >= L - 1) return li;
-  if (h->s1_form != 1 && !(h->s1_form == 2 && h->layers[li].h_in <= 16)) return li;
+  if (h->s1_form != 1) return li;
   auto s1_64 = [&](int i) {
     const LayerDef& d = h->layers[i].def;
     return d.kind == K_S1 && d.cin == 64 && d.cout == 64 && i > 0 && i < L - 1;
@@ -741,7 +737,7 @@ static int chain_end(const tic_handle* h, int li) {
   if (!first_dec && s1_64(li - 1) && (h->rmbe() || li - 1 != h->n_enc - 1)) return li;  // not a run start
   int j = li + 1;
   while (j < L - 1 && j - li < tic::CH_MAX_LAYERS && s1_64(j) && (h->rmbe() || j != h->n_enc)) ++j;
-  if (h->s1_form == 1) {
+  {
     // Geometry the region chain can run: a region keeps its workgroup for all nl
     // layers, and to publish layer k region t needs layer k-1 of region t + rw + 1, which needs
     // layer k-2 of t + 2 (rw + 1) ...: min(R, (nl - 1)(rw + 1) + 1) workgroups of a patch must
@@ -751,9 +747,8 @@ static int chain_end(const tic_handle* h, int li) {
     // n <= chunk) must fit the 32-bit buffer-resource range.
     const int rw = (h->layers[li].h_in + 7) / 8;
     const long R = (long)rw * rw;
-    const int per_region = h->chain_wh >= 3 ? 2 : 1;  // workgroups per region
-    const long slots = (long)h->num_cus * (h->chain_wh == 2 || h->chain_wh == 4 ? 1 : 2);
-    auto need = [&](int nl) { return 2L * h->nlanes * per_region * std::min(R, (long)(nl - 1) * (rw + 1) + 1); };
+    const long slots = (long)h->num_cus * (h->chain_wh == 2 ? 1 : 2);
+    auto need = [&](int nl) { return 2L * h->nlanes * std::min(R, (long)(nl - 1) * (rw + 1) + 1); };
     while (j - li >= 2 && need(j - li) > slots) --j;
     if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
   }
@@ -761,7 +756,6 @@ static int chain_end(const tic_handle* h, int li) {
   // chain keeps a block input it read in LDS only, so the block's residual conv must run in
   // the same launch (after a run, the per-layer path has no block input in a workspace)
   while (j - li >= 2 && h->layers[j].def.residual) --j;
-  // (form 2: four workgroups of a patch wait for each other; one per CU is always resident)
   return j - li >= 2 ? j : li;
 }
 // layer i runs inside some wino_chain_kernel launch
@@ -916,16 +910,13 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
     if (ce > li && ce <= l1) {
       const int nl = ce - li;
       const bool last_enc_c = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      const bool pc = pchain_form(h, li);
-      // hand-off buffers: 8x8 regions (form 1), or four channel quarters per patch, whose
-      // 16 KB slices take the room of four regions' records
-      const int R = pc ? 4 : ((lay.h_in + 7) / 8) * ((lay.h_in + 7) / 8);
+      const int R = ((lay.h_in + 7) / 8) * ((lay.h_in + 7) / 8);  // 8x8 regions per patch
       int rc = ensure_chain(h, ln, nl, n, R);
       if (rc) return rc;
       tic::ChainArgs a{};
       for (int k = 0; k < nl; ++k) {
         const LayerRT& lk = h->layers[li + k];
-        a.layer[k] = {pc ? lk.d_ww4 : lk.d_ww, lk.d_b, lk.def.act, lk.def.residual};
+        a.layer[k] = {lk.d_ww, lk.d_b, lk.def.act, lk.def.residual};
       }
       a.nl = nl;
       a.in = first_dec ? in : (const void*)src;
@@ -942,11 +933,11 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.dispatch_order = h->chain_order;
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
-        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R * (!pc && h->chain_wh >= 3 ? 2 : 1), st, &a.tstamp);
+        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R, st, &a.tstamp);
         if (rc2) return rc2;
       }
       const int inm = first_dec ? tic::IN_IDX : tic::IN_F32, outm = last_enc_c ? tic::OUT_QUANT : tic::OUT_F32;
-      if (pc ? !tic::launch_wino4_pchain(inm, outm, a, st) : !tic::launch_wino_chain(inm, outm, a, st, h->chain_wh))
+      if (!tic::launch_wino_chain(inm, outm, a, st, h->chain_wh))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);
       rc = check_launch();
       if (rc) return rc;
@@ -1326,7 +1317,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE01")) h->fuse01 = atoi(f) != 0;
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
-  if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(4, std::max(1, atoi(f)));
+  if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(2, std::max(1, atoi(f)));
   if (const char* f = getenv("TIC_CHAIN_ORDER")) h->chain_order = atoi(f) != 0;
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -1703,8 +1694,8 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->chain = value < 0 ? struct_defaults(h->model_id).chain : value != 0;
     return TIC_OK;
   }
-  if (k == "chain_wh") {  // chain workgroup: 1 = 256 threads, 2 = 512, 3 / 4 = two 256- / 512-thread halves per region
-    if (value < 1 || value > 4) return fail(TIC_EINVAL, "chain_wh must be 1..4");
+  if (k == "chain_wh") {  // chain workgroup: 1 = 256 threads, 2 = 512
+    if (value < 1 || value > 2) return fail(TIC_EINVAL, "chain_wh must be 1 or 2");
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->chain_wh = value;
@@ -2018,10 +2009,10 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     float alt = 1e30f;
     if (f.v == &h->chain && !was && !getenv("TIC_CHAIN_WH") && h->s1_form == 1) {
       // switching the chain on: in each of its workgroup shapes (whether it pays depends on
-      // the shape: the channel-split ones double the workgroups of small stages)
+      // the shape)
       const int wh0 = h->chain_wh;
       int best_wh = wh0;
-      for (int wh = 1; wh <= 4 && !rc; ++wh) {
+      for (int wh = 1; wh <= 2 && !rc; ++wh) {
         h->chain_wh = wh;
         clear_graphs(h);
         if (!any_chain(h)) continue;
@@ -2057,7 +2048,7 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
   if (!rc && h->chain && any_chain(h) && !getenv("TIC_CHAIN_WH") && h->s1_form == 1) {  // the region chain's shape
     const int was = h->chain_wh;
     int best_wh = was;
-    for (int wh = 1; wh <= 4 && !rc; ++wh) {
+    for (int wh = 1; wh <= 2 && !rc; ++wh) {
       if (wh == was) continue;
       h->chain_wh = wh;
       clear_graphs(h);
@@ -2214,13 +2205,7 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     if (cs == i) {
       const int ce = chain_end(h, cs);
       const bool first_dec = !h->rmbe() && cs == h->n_enc, last_enc = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      if (pchain_form(h, cs))
-        snprintf(buf, sizeof buf, "wino4_pchain_kernel<%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0);
-      else if (h->chain_wh >= 3)
-        snprintf(buf, sizeof buf, "wino_chain_cs_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0,
-                 h->chain_wh - 2);
-      else
-        snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh);
+      snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh);
     }
   } else if (fuses_tail(h) && i >= L - 2) {
     if (i == L - 2) {
@@ -2267,9 +2252,6 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     else if (e->wlds == 4)
       snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
                e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
-    else if (e->wlds == 3)
-      snprintf(buf, sizeof buf, "conv3x3_persist_kernel<%d,%d,%d,%d,%d,%d>", e->mode, e->cin, e->cout, e->th, e->wr,
-               e->act);
     else
       snprintf(buf, sizeof buf, "conv3x3<%d,%d,%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th,
                e->wr, e->nsplit, e->wlds, e->act, tf[e->res != 0], e->in, e->out);
@@ -2333,7 +2315,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
       else if (!strcmp(name, "s1_form") && a >= 0 && a <= 2) s1_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
-      else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 4) chain_wh = a;
+      else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 2) chain_wh = a;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
     } else if (!strcmp(kind, "conv")) {
       if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)
