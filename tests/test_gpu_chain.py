@@ -122,3 +122,25 @@ def test_wino_chain_device_path_and_tuning_replay():
                 with pytest.raises(ValueError):
                     c2.tuning_import("tic-tuning 1\n" + bad + "\n")
             assert c2.tuning_export() == text  # nothing applied by the rejected imports
+
+
+def test_chain_cut_inside_res_block_fails_loudly(monkeypatch):
+    """a chain run that ends inside a res_block keeps the block input in
+    LDS only, so the block's residual conv that follows unfused has no block input in a
+    workspace.  The planner never makes such a run (round 4's P = 4096 page fault was one);
+    forced through the test hook, the call must fail with TIC_EINVAL ("residual input not in
+    a workspace") instead of launching that conv on workspace -1.  Reference:
+    basic_block/basic_block.py:74-93 (the residual add of res_block)."""
+    x = structured_patches(2, 256, seed=720)
+    with _codec(0, 256) as c:
+        c.set_option("s1_form", 1)
+        c.set_option("chain", 1)
+        c.set_option("streams", 1)
+        ref = c.encode(x)
+        # model_0 encoder run: res_1/conv_0, res_1/conv_1, res_2/conv_0 | res_2/conv_1 ...
+        monkeypatch.setenv("TIC_TEST_CHAIN_CUT", "3")
+        with pytest.raises(ValueError, match=r"\[EINVAL\].*residual input not in a workspace"):
+            c.encode(x)
+        monkeypatch.delenv("TIC_TEST_CHAIN_CUT")
+        c.synchronize()
+        assert np.array_equal(c.encode(x), ref)  # the handle stays usable

@@ -752,6 +752,12 @@ static int chain_end(const tic_handle* h, int li) {
     while (j - li >= 2 && need(j - li) > slots) --j;
     if ((size_t)h->chunk * rw * rw * 16384 > (size_t)INT_MAX) return li;
   }
+  // test hook (tests/test_gpu_chain.py): runs cut to this many layers WITHOUT the guard
+  // below, so run_layers' own check of a residual conv without its block input is reached
+  if (const char* t = getenv("TIC_TEST_CHAIN_CUT")) {
+    j = std::min(j, li + atoi(t));
+    return j - li >= 2 ? j : li;
+  }
   // A run cut short (residency above, or CH_MAX_LAYERS) never ends inside a res_block: the
   // chain keeps a block input it read in LDS only, so the block's residual conv must run in
   // the same launch (after a run, the per-layer path has no block input in a workspace)
@@ -1963,6 +1969,47 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     return TIC_OK;
   };
   const bool log = getenv("TIC_TUNE_LOG") != nullptr;
+  // Alternating A/B of the current state against an alternative (apply(true) installs the
+  // alternative, apply(false) the current state): kPairs pairs, the order inside a pair
+  // alternating, so clock drift and the GPU's warm-up cannot favour either side.  The
+  // alternative is kept only if it is faster in EVERY pair and by more than `margin` in the
+  // median pair (one-shot comparisons flipped structural decisions
+  // between fresh runs).  On return the winner is installed; *cur_ms = its median time.
+  constexpr int kPairs = 3;
+  // a per-layer candidate enters the A/B only if its sweep time beats the best so far by this
+  constexpr float kSweepMargin = 0.003f;
+  auto confirm = [&](const std::function<void(bool)>& apply, float margin, const char* what, bool* keep,
+                     float* cur_ms) -> int {
+    float a[kPairs], b[kPairs];
+    int wins = 0;
+    for (int k = 0; k < kPairs; ++k) {
+      for (int side = 0; side < 2; ++side) {
+        const bool alt_side = (side == 0) == (k % 2 == 1);  // pairs: (base, alt), (alt, base), ...
+        apply(alt_side);
+        clear_graphs(h);
+        int r = measure(alt_side ? &a[k] : &b[k]);
+        if (r) {
+          apply(false);
+          clear_graphs(h);
+          return r;
+        }
+      }
+      if (a[k] < b[k]) ++wins;
+    }
+    float ra[kPairs], rb[kPairs], ratio[kPairs];
+    for (int k = 0; k < kPairs; ++k) ratio[k] = a[k] / b[k], ra[k] = a[k], rb[k] = b[k];
+    std::sort(ratio, ratio + kPairs);
+    std::sort(ra, ra + kPairs);
+    std::sort(rb, rb + kPairs);
+    *keep = wins == kPairs && ratio[kPairs / 2] < 1.f - margin;
+    if (log)
+      fprintf(stderr, "tune-step A/B %s: alternative %.2f us vs current %.2f us (median), wins %d/%d: %s\n", what,
+              1e3f * ra[kPairs / 2], 1e3f * rb[kPairs / 2], wins, kPairs, *keep ? "switch" : "keep");
+    apply(*keep);
+    clear_graphs(h);
+    *cur_ms = *keep ? ra[kPairs / 2] : rb[kPairs / 2];
+    return TIC_OK;
+  };
   // test hooks (tests/test_gpu_tuning.py): "flip" accepts every structural alternative (the
   // fusions and the chain switch state whatever they measure), "nowin" lets no per-layer
   // candidate win — together they reach layers that were never tuned and keep no candidate
@@ -2004,14 +2051,19 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     const bool can = f.applies(h);
     *f.v = was;
     if (!can) continue;
-    *f.v = !was;
-    clear_graphs(h);
-    float alt = 1e30f;
+    if (t_flip) {
+      *f.v = !was;
+      clear_graphs(h);
+      continue;
+    }
+    bool keep = false;
     if (f.v == &h->chain && !was && !getenv("TIC_CHAIN_WH") && h->s1_form == 1) {
-      // switching the chain on: in each of its workgroup shapes (whether it pays depends on
-      // the shape)
+      // switching the chain on: in its better workgroup shape (one quick measurement each to
+      // pick the shape, then the confirmed A/B of that shape against the chain off)
       const int wh0 = h->chain_wh;
       int best_wh = wh0;
+      float best_m = 1e30f;
+      h->chain = true;
       for (int wh = 1; wh <= 2 && !rc; ++wh) {
         h->chain_wh = wh;
         clear_graphs(h);
@@ -2019,49 +2071,25 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
         float m = 0.f;
         rc = measure(&m);
         if (log && !rc) fprintf(stderr, "tune-step chain=1 chain_wh=%d : %.2f us\n", wh, 1e3f * m);
-        if (!rc && m < alt) {
-          alt = m;
-          best_wh = wh;
-        }
+        if (!rc && m < best_m) best_m = m, best_wh = wh;
       }
-      h->chain_wh = alt < cur ? best_wh : wh0;
-    } else {
-      // the current state re-timed right before the alternative (clock drift between two
-      // distant measurements must not decide a structural switch), and the switch kept only
-      // for a gain above 0.5 %
-      *f.v = was;
-      clear_graphs(h);
-      float base = 0.f;
-      rc = measure(&base);
-      if (!rc) cur = base;
-      *f.v = !was;
-      clear_graphs(h);
-      if (!rc) rc = measure(&alt);
-      if (log && !rc) fprintf(stderr, "tune-step %s=%d : %.2f us (current %.2f)\n", f.name, (int)*f.v, 1e3f * alt,
-                              1e3f * base);
-      if (!rc && !t_flip && alt >= 0.995f * base) alt = 1e30f;
+      h->chain = was;
+      h->chain_wh = best_wh;
+      if (!rc)
+        rc = confirm([&](bool alt) { h->chain = alt ? !was : was; h->chain_wh = alt ? best_wh : wh0; }, 0.005f,
+                     "chain", &keep, &cur);
+    } else if (!rc) {
+      rc = confirm([&](bool alt) { *f.v = alt ? !was : was; }, 0.005f, f.name, &keep, &cur);
     }
-    if (!rc && (alt < cur || t_flip)) cur = alt;
-    else *f.v = was;
     clear_graphs(h);
   }
   if (!rc && h->chain && any_chain(h) && !getenv("TIC_CHAIN_WH") && h->s1_form == 1) {  // the region chain's shape
-    const int was = h->chain_wh;
-    int best_wh = was;
-    for (int wh = 1; wh <= 2 && !rc; ++wh) {
-      if (wh == was) continue;
-      h->chain_wh = wh;
-      clear_graphs(h);
-      if (!any_chain(h)) continue;  // this shape's geometry check declines the chain
-      float alt = 0.f;
-      rc = measure(&alt);
-      if (log && !rc) fprintf(stderr, "tune-step chain_wh=%d : %.2f us\n", wh, 1e3f * alt);
-      if (!rc && alt < cur) {
-        cur = alt;
-        best_wh = wh;
-      }
-    }
-    h->chain_wh = best_wh;
+    const int was = h->chain_wh, other = 3 - was;
+    h->chain_wh = other;
+    const bool fits = any_chain(h);  // this shape's geometry check may decline the chain
+    h->chain_wh = was;
+    bool keep = false;
+    if (fits) rc = confirm([&](bool alt) { h->chain_wh = alt ? other : was; }, 0.005f, "chain_wh", &keep, &cur);
     clear_graphs(h);
   }
   const int L = (int)h->layers.size();
@@ -2089,13 +2117,18 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
           float ms = 0.f;
           rc = measure(&ms);
           if (log) fprintf(stderr, "tune-step %s variant %d : %.2f us\n", tail ? "dec10" : "enc01", v, 1e3f * ms);
-          if (!rc && ms < best) {
+          if (!rc && ms < best * (1.f - kSweepMargin)) {
             best = ms;
             best_v = v;
           }
         }
-        for (int m : sizes) l.tuned_var[sg * m] = best_v;
-        cur = best;
+        auto put = [&](int v) {
+          for (int m : sizes) l.tuned_var[sg * m] = v;
+        };
+        put(keep);
+        bool sw = false;
+        if (!rc && best_v != keep)
+          rc = confirm([&](bool alt) { put(alt ? best_v : keep); }, kSweepMargin, tail ? "dec10" : "enc01", &sw, &cur);
         continue;
       }
       if (first || last) {
@@ -2111,13 +2144,18 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
           float ms = 0.f;
           rc = measure(&ms);
           if (log) fprintf(stderr, "tune-step %-22s variant %d : %.2f us\n", d.name.c_str(), v, 1e3f * ms);
-          if (!rc && ms < best) {
+          if (!rc && ms < best * (1.f - kSweepMargin)) {
             best = ms;
             best_v = v;
           }
         }
-        for (int m : sizes) l.tuned_var[m] = best_v;
-        cur = best;
+        auto put = [&](int v) {
+          for (int m : sizes) l.tuned_var[m] = v;
+        };
+        put(keep);
+        bool sw = false;
+        if (!rc && best_v != keep)
+          rc = confirm([&](bool alt) { put(alt ? best_v : keep); }, kSweepMargin, d.name.c_str(), &sw, &cur);
       } else {
         const bool last_enc = !h->rmbe() && i == h->n_enc - 1, first_dec = !h->rmbe() && i == h->n_enc;
         const int hg = d.kind == K_T2 ? l.h_in : l.h_out;
@@ -2137,16 +2175,21 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
           if (log)
             fprintf(stderr, "tune-step %-22s th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), c->th, c->nsplit,
                     c->wlds, 1e3f * ms);
-          if (!rc && ms < best && !t_nowin) {
+          if (!rc && ms < best * (1.f - kSweepMargin) && !t_nowin) {
             best = ms;
             best_e = c;
           }
         }
-        for (int m : sizes) {
-          if (best_e) l.tuned[tkey(h, l, m)] = best_e;
-          else l.tuned.erase(tkey(h, l, m));
-        }
-        cur = best;
+        auto put = [&](const tic::ConvEntry* e) {
+          for (int m : sizes) {
+            if (e) l.tuned[tkey(h, l, m)] = e;
+            else l.tuned.erase(tkey(h, l, m));
+          }
+        };
+        put(keep);
+        bool sw = false;
+        if (!rc && best_e != keep)
+          rc = confirm([&](bool alt) { put(alt ? best_e : keep); }, kSweepMargin, d.name.c_str(), &sw, &cur);
       }
     }
     if (log && !rc) fprintf(stderr, "tune-step n=%d after round %d: %.2f us\n", n, round + 1, 1e3f * cur);
