@@ -517,6 +517,14 @@ def main():
     roof["kernel_instance"] = dom_kernels
     roof["launches_per_step_per_lane"] = dom["launches"]
     roof["ms_per_launch"] = round(dom_ms, 5)
+    if len(members) > 1:
+        # the family mean spans several instances (e.g. model_3's F(4x4,3x3) conv at three
+        # tilings and two map sizes): the roofline of its largest member beside it
+        big = max(members, key=lambda k: groups[k]["ms"] / groups[k]["launches"])
+        rb, rbms, _, _ = roofline_of(groups[big], lane_b)
+        roof["largest_member"] = {"kernel": "+".join(groups[big]["layers"]),
+                                  "kernel_instance": sorted({kernels[names[nm]] for nm in groups[big]["layers"]} - {""}),
+                                  "ms_per_launch": round(rbms, 5), "achieved": rb["achieved"], "frac": rb["frac"]}
     if top_in_step is not None and top_in_step not in members:  # for the record
         r1, ms1, _, _ = roofline_of(groups[top_in_step], lane_b)
         gi = dict(groups[top_in_step])

@@ -397,6 +397,9 @@ static void launch_wino4(const ConvArgs& a, int n, hipStream_t s) {
     if (a.qout) b.qout = a.qout + (size_t)n0 * a.Ho * a.Wo * COUT;
     if (a.res) b.res = a.res + (size_t)n0 * a.Ho * a.Wo * COUT;
     dim3 grid((a.Wo + OW - 1) / OW, (a.Ho + OH - 1) / OH, std::min(step, n - n0));
+    // timing probe: every split launch restarts blockIdx.z at 0, so its stamps go after the
+    // workgroups of the launches before it
+    if (a.tstamp) b.tstamp = a.tstamp + (size_t)TIC_W4_TS * grid.x * grid.y * n0;
     hipLaunchKernelGGL((conv3x3_wino4_kernel<CIN, COUT, TTY, ACT, RES, IN, OUT>), grid, dim3(768), 0, s, b);
   }
 }

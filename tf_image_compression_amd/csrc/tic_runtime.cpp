@@ -2532,8 +2532,9 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   a.num_cus = h->num_cus;
   a.grid_cap = h->persist_grid;
   a.max_n = h->wino4_max_n;
-  // timing probe of the F(4x4,3x3) kernel (tools/wino4_timing.py): [workgroup][8] stamps,
-  // appended to the file TIC_WINO4_TIMING names as {grid words, stamps}
+  // timing probe of the F(4x4,3x3) kernel (tools/wino4_timing.py): [workgroup][TIC_W4_TS]
+  // stamps (split launches write after each other), appended to the file TIC_WINO4_TIMING
+  // names as {grid words, stamps}
   const char* tpath = e->wlds == 5 ? getenv("TIC_WINO4_TIMING") : nullptr;
   Scratch s_ts;
   const size_t nwg = (size_t)n * ((a.Ho + 3) / 4) * ((a.Wo + 3) / 4);  // >= the launch's workgroups
