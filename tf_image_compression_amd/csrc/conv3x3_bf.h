@@ -28,13 +28,18 @@
 //     M3: A = [w2 | w0], B = T2 = [x0 | x2]  -> w2 x0 + w0 x2
 // issued M3, M2, M1 (small terms first).
 //
-// LDS activation tile: per (pixel, channel quad) a 24-byte record [x1 | x0 | x2] (4 bf16
-// each; 1.5x the f32 tile), split once at staging; a step reads it with three ds_read_b64
-// and forms T1 / T2 in registers.  Pixel stride 6 Cin/4 + 4 dwords: the ds_read_b64 of 16
-// pixels x 4 lane groups is conflict-free in both 32-lane halves.
-// Weights: packed on the host as [tap][Cin/16][4 lg][Cout][w0 | w1 | w2] (4 bf16 each, 24
-// bytes per lane and step: three 8-byte buffer loads), from L2 into registers two steps
-// ahead; the tuples A1..A3 are register copies.
+// LDS activation tile: per (pixel, channel quad) the two B tuples T1 = [x1 | x0] and
+// T2 = [x0 | x2] (4 bf16 each half), split once at staging — per 16-channel chunk the 32
+// dwords [T1 of lane groups 0..3 | T2 of lane groups 0..3]; a step reads them with two
+// ds_read_b128 that land in the MFMA operand registers as they are (an operand tuple built
+// by register copies cost the first build four v_mov per MFMA).  Pixel stride 2 Cin + 8
+// dwords (= 8 mod 16): conflict-free in every 16-lane group of ds_read_b128.
+// Weights: per (tap, output-channel split) a slab [Cin/16][4 lg][Cout/NSPLIT] of the three A
+// tuples [w0 | w0], [w1 | w1], [w2 | w0] (12 dwords; row pitch 12 Cout/NSPLIT = 0 mod 64:
+// conflict-free), fetched once per workgroup by LDS-DMA one tap ahead into a 2-slot ring
+// (WSRC 1), or per wave from L2 PF = 4 steps ahead (WSRC 0, small grids / large slabs).
+// Why the ring: with the matrix time cut 2.67x, four waves each fetching the same weight
+// fragments through the CU's 64 B/clk load path became the bound.
 #pragma once
 #include "conv3x3.h"
 
@@ -70,13 +75,13 @@ __device__ __forceinline__ void bf_split4(f32x4 v, u32x2_t& x0, u32x2_t& x1, u32
 
 template <int CIN>
 struct BfTile {
-  static constexpr int REC = 6;                  // dwords per (pixel, quad) record
-  static constexpr int PS = REC * CIN / 4 + 4;   // dwords per pixel (conflict-free b64 reads)
+  static constexpr int PS = 2 * CIN + 8;  // dwords per pixel: 8 per channel quad + 8
 };
 
-template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, int ACT, bool RES, int IN, int OUT>
+template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, int WSRC, int ACT, bool RES, int IN, int OUT>
 __global__ void __launch_bounds__(256) conv3x3_bf_kernel(const ConvArgs a) {
   static_assert(CIN % 16 == 0 && COUT % 16 == 0, "channels must be multiples of 16");
+  constexpr bool WLDS = WSRC == 1;
   constexpr int PS = BfTile<CIN>::PS;
   constexpr int KC = CIN / 16;
   constexpr int COUT_WG = COUT / NSPLIT;
@@ -91,9 +96,13 @@ __global__ void __launch_bounds__(256) conv3x3_bf_kernel(const ConvArgs a) {
   constexpr int LC = TileGeom<MODE, TH>::LC;
   constexpr int C4 = CIN / 4;
   constexpr int NSTEP = 9 * KC;
-  constexpr int TILE = LR * LC * PS;  // dwords of the input tile
+  constexpr int TILE = LR * LC * PS;       // dwords of the input tile
+  constexpr int RP = bf_wpitch(COUT_WG);   // weight row pitch (dwords), 12 COUT_WG
+  constexpr int SLAB = KC * 4 * RP;        // dwords of one tap's weights for this split
+  static_assert(SLAB % 4 == 0, "slab of 16-byte chunks");
+  constexpr int SCH = SLAB / 4;            // 16-byte chunks per slab
 
-  __shared__ __attribute__((aligned(16))) unsigned smem[TILE];
+  __shared__ __attribute__((aligned(16))) unsigned smem[TILE + (WLDS ? 2 * SLAB : 0)];
 
   const int tid = threadIdx.x;
   const int split = NSPLIT > 1 ? (int)(blockIdx.x % NSPLIT) : 0;
@@ -111,26 +120,52 @@ __global__ void __launch_bounds__(256) conv3x3_bf_kernel(const ConvArgs a) {
   const int co_wg = split * COUT_WG;
   const int co_wave = wc * NB * 16;
 
-  // ---- weights: [tap][kc][lg][COUT][6 dwords] -> w0, w1, w2 of this lane's channels ----
-  const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(a.wp, 9 * KC * 4 * COUT * 24);
-  const int wlb = (lg * COUT + co_wg + co_wave + li) * 24;  // lane byte offset
+  // ---- weights: slab of (tap, split) at dword ((tap * NSPLIT + split) * SLAB); inside it the
+  //      A tuples of (kc, lg, co_local) at (kc * 4 + lg) * RP + co_local * 12 ----
+  const unsigned* const wsrc = reinterpret_cast<const unsigned*>(a.wp) + (size_t)split * SLAB;
   struct W3 {
-    u32x2_t p[3];
+    wu32x4 t[3];
   };
+  const int wlane = lg * RP + (co_wave + li) * 12;  // this lane's record offset in a (kc) row block
+  auto wdma = [&](int tap, int slot) {  // LDS-DMA one tap slab
+#pragma unroll
+    for (int j = 0; j < (SCH + 255) / 256; ++j) {
+      const int cbase = (j * 4 + wave) * 64;
+      if (SCH % 256 == 0 || cbase < SCH) {
+        const unsigned* src = wsrc + (size_t)tap * NSPLIT * SLAB + (cbase + lane) * 4;
+        if (SCH % 64 == 0 || cbase + lane < SCH)
+          __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(smem + TILE + slot * SLAB + cbase * 4), 16, 0, 0);
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(a.wp, 9 * NSPLIT * SLAB * 4);
   auto wglob = [&](int s, int nb) -> W3 {
-    const int so = (s * 4 * COUT + nb * 16) * 24;
+    const int tap = s / KC, kc = s % KC;
+    const int so = ((tap * NSPLIT) * SLAB + kc * 4 * RP + nb * 16 * 12) * 4;
     W3 w;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) w.p[q] = __builtin_amdgcn_raw_buffer_load_b64(wrs, wlb, so + 8 * q, 0);
+    for (int q = 0; q < 3; ++q) w.t[q] = __builtin_amdgcn_raw_buffer_load_b128(wrs, (split * SLAB + wlane) * 4, so + 16 * q, 0);
     return w;
   };
-  constexpr int PF = 2;
+  auto wlds = [&](int s, int nb) -> W3 {
+    const int tap = s / KC, kc = s % KC;
+    const unsigned* r = &smem[TILE + (tap & 1) * SLAB + kc * 4 * RP + wlane + nb * 16 * 12];
+    W3 w;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) w.t[q] = *reinterpret_cast<const wu32x4*>(r + 4 * q);
+    return w;
+  };
+  constexpr int PF = WLDS ? 1 : 4;
   W3 av[PF + 1][NB];
+  if constexpr (WLDS) {
+    wdma(0, 0);
+  } else {
 #pragma unroll
-  for (int p = 0; p < PF; ++p)
+    for (int p = 0; p < PF; ++p)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-      if (p < NSTEP) av[p][nb] = wglob(p, nb);
+      for (int nb = 0; nb < NB; ++nb)
+        if (p < NSTEP) av[p][nb] = wglob(p, nb);
+  }
 
   // ---- stage the input tile: f32 (or dequantised symbols) -> three bf16 parts ----
   constexpr int NSTAGE = LR * LC * C4;
@@ -181,13 +216,14 @@ __global__ void __launch_bounds__(256) conv3x3_bf_kernel(const ConvArgs a) {
         const int c4 = e % C4, pe = e / C4;
         u32x2_t x0, x1, x2;
         bf_split4(tmp[i], x0, x1, x2);
-        unsigned* r = &smem[pe * PS + c4 * 6];
-        *reinterpret_cast<u32x2_t*>(r) = x1;
-        *reinterpret_cast<u32x2_t*>(r + 2) = x0;
-        *reinterpret_cast<u32x2_t*>(r + 4) = x2;
+        // chunk c4 / 4, lane group c4 % 4: T1 at slot (c4 % 4), T2 at slot 4 + (c4 % 4)
+        unsigned* r = &smem[pe * PS + (c4 >> 2) * 32 + (c4 & 3) * 4];
+        *reinterpret_cast<wu32x4*>(r) = wu32x4{x1.x, x1.y, x0.x, x0.y};
+        *reinterpret_cast<wu32x4*>(r + 16) = wu32x4{x0.x, x0.y, x2.x, x2.y};
       }
     }
   }
+  if constexpr (WLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   f32x4 acc[NPH][MB][NB];
@@ -198,9 +234,9 @@ __global__ void __launch_bounds__(256) conv3x3_bf_kernel(const ConvArgs a) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[p][mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // this lane's parts of step s (pixel row mb): x1, x0, x2 of its channel quad
+  // this lane's B tuples of step s (pixel row mb): T1 = [x1 | x0], T2 = [x0 | x2]
   struct X3 {
-    u32x2_t p1, p0, p2;
+    wu32x4 t1, t2;
   };
   auto load_b = [&](int s, X3* dst) {
     const int tap = s / KC, kc = s % KC;
@@ -212,47 +248,64 @@ __global__ void __launch_bounds__(256) conv3x3_bf_kernel(const ConvArgs a) {
       if constexpr (MODE == MODE_S1) lp = (r + ky) * LC + li + kx;
       else if constexpr (MODE == MODE_S2) lp = (2 * r + ky) * LC + (kx & 1) * 17 + li + (kx >> 1);
       else lp = (r + 1 - (ky == 2)) * LC + li + 1 - (kx == 2);
-      const unsigned* rec = &smem[lp * PS + (kc * 4 + lg) * 6];
-      dst[mb].p1 = *reinterpret_cast<const u32x2_t*>(rec);
-      dst[mb].p0 = *reinterpret_cast<const u32x2_t*>(rec + 2);
-      dst[mb].p2 = *reinterpret_cast<const u32x2_t*>(rec + 4);
+      const unsigned* rec = &smem[lp * PS + kc * 32 + lg * 4];
+      dst[mb].t1 = *reinterpret_cast<const wu32x4*>(rec);
+      dst[mb].t2 = *reinterpret_cast<const wu32x4*>(rec + 16);
     }
   };
 
   X3 bx[2][MB];
   load_b(0, bx[0]);
+  if constexpr (WLDS) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) av[0][nb] = wlds(0, nb);
+  }
 #pragma unroll
   for (int s = 0; s < NSTEP; ++s) {
-    const int tap = s / KC;
+    const int tap = s / KC, kc = s % KC;
     const int ky = tap / 3, kx = tap % 3;
     const int c = s & 1;
-    if (s + PF < NSTEP) {
+    if constexpr (WLDS) {
+      if (kc == 0 && tap + 1 < 9) wdma(tap + 1, (tap + 1) & 1);
+    } else if (s + PF < NSTEP) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) av[(s + PF) % (PF + 1)][nb] = wglob(s + PF, nb);
     }
-    if (s + 1 < NSTEP) load_b(s + 1, bx[c ^ 1]);
+    // the next step's LDS fragments (within a tap: the slot is already resident)
+    const bool pre = s + 1 < NSTEP && !(WLDS && kc == KC - 1);
+    if (pre) {
+      load_b(s + 1, bx[c ^ 1]);
+      if constexpr (WLDS) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) av[c ^ 1][nb] = wlds(s + 1, nb);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     const int ph = MODE == MODE_T2 ? (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0) : 0;
-    const int wi = s % (PF + 1);
+    const int wi = WLDS ? c : s % (PF + 1);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const W3& w = av[wi][nb];
-      const wu32x4 a1 = {w.p[0].x, w.p[0].y, w.p[0].x, w.p[0].y};
-      const wu32x4 a2 = {w.p[1].x, w.p[1].y, w.p[1].x, w.p[1].y};
-      const wu32x4 a3 = {w.p[2].x, w.p[2].y, w.p[0].x, w.p[0].y};
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
         const X3& x = bx[c][mb];
-        const wu32x4 t1 = {x.p1.x, x.p1.y, x.p0.x, x.p0.y};
-        const wu32x4 t2 = {x.p0.x, x.p0.y, x.p2.x, x.p2.y};
         f32x4 v = acc[ph][mb][nb];
-        v = mfma_bf(a3, t2, v);
-        v = mfma_bf(a2, t1, v);
-        v = mfma_bf(a1, t1, v);
+        v = mfma_bf(w.t[2], x.t2, v);
+        v = mfma_bf(w.t[1], x.t1, v);
+        v = mfma_bf(w.t[0], x.t1, v);
         acc[ph][mb][nb] = v;
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WLDS) {
+      if (kc == KC - 1 && tap + 1 < 9) {  // the next tap's slab has landed (one barrier per tap)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        load_b(s + 1, bx[c ^ 1]);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) av[c ^ 1][nb] = wlds(s + 1, nb);
+      }
+    }
   }
 
   // ---- fused epilogue (conv3x3_kernel's): + bias, act, + residual, f32 store or quantiser ----

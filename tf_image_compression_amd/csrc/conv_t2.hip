@@ -39,7 +39,7 @@ static const ConvEntry kT2[] = {
     TIC_CONVBF(MODE_T2, 64, 64, 2, 2, 2, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONVBF(MODE_T2, 64, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
     TIC_CONVBF(MODE_T2, 80, 64, 2, 2, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_CONVBF(MODE_T2, 80, 64, 4, 4, 1, ACT_ID, false, IN_IDX, OUT_F32),
+    TIC_CONVBFW(MODE_T2, 80, 64, 4, 4, 1, 0, ACT_ID, false, IN_IDX, OUT_F32),
 };
 const ConvEntry* conv_registry_t2(int* count) {
   *count = sizeof(kT2) / sizeof(kT2[0]);

@@ -175,7 +175,7 @@ int same_pad(int kind, int h) {
 // (weight source 5), 3 the direct form with its f32 products on the bf16 matrix path
 // (conv3x3_bf.h, weight source 6), else 0 (direct, f32 MFMA)
 int entry_form(const tic::ConvEntry& c) {
-  return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : (c.wlds == 6 ? 3 : 0));
+  return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : (c.wlds == 6 || c.wlds == 7 ? 3 : 0));
 }
 
 // F(4x4,3x3) stages a patch through 32-bit buffer byte offsets: a patch (input or output) of
@@ -291,11 +291,14 @@ float bf16_val(uint16_t h) {
   return f;
 }
 
-// conv3x3_bf.h weights from the generic packing: [tap][Cin/16][4 lg][Cout][3 parts][4 t]
-// bf16 (ci = 16 kc + 4 lg + t), the parts w0 = rne(w), w1 = rne(w - w0), w2 = rne(w - w0 - w1)
-void pack_bf(const std::vector<float>& wp, int cin, int cout, std::vector<uint16_t>* out) {
-  const int KC = cin / 16;
-  out->assign((size_t)9 * cin * cout * 3, 0);
+// conv3x3_bf.h weights from the generic packing (ci = 16 kc + 4 lg + t): per (tap, output-
+// channel split) a slab [Cin/16][4 lg][Cout/nsplit records of the three A tuples
+// [w0 | w0], [w1 | w1], [w2 | w0] (4 t each half, 24 bf16)], rows of tic::bf_wpitch dwords;
+// the parts w0 = rne(w), w1 = rne(w - w0), w2 = rne(w - w0 - w1) sum to w exactly
+void pack_bf(const std::vector<float>& wp, int cin, int cout, int nsplit, std::vector<uint16_t>* out) {
+  const int KC = cin / 16, cw = cout / nsplit, rp = tic::bf_wpitch(cw);  // rp in dwords
+  const size_t slab = (size_t)KC * 4 * rp * 2;                             // uint16 per slab
+  out->assign((size_t)9 * nsplit * slab, 0);
   for (int tap = 0; tap < 9; ++tap)
     for (int kc = 0; kc < KC; ++kc)
       for (int g = 0; g < 4; ++g)
@@ -306,10 +309,14 @@ void pack_bf(const std::vector<float>& wp, int cin, int cout, std::vector<uint16
             const float r = w - bf16_val(p0);
             const uint16_t p1 = bf16_rne(r);
             const uint16_t p2 = bf16_rne(r - bf16_val(p1));
-            const size_t o = ((((size_t)tap * KC + kc) * 4 + g) * cout + co) * 12 + t;
-            (*out)[o] = p0;
-            (*out)[o + 4] = p1;
-            (*out)[o + 8] = p2;
+            const int sp = co / cw, cl = co % cw;
+            const size_t o = ((size_t)tap * nsplit + sp) * slab + ((size_t)kc * 4 + g) * rp * 2 + (size_t)cl * 24 + t;
+            (*out)[o] = p0;        // A1 = [w0 | w0]
+            (*out)[o + 4] = p0;
+            (*out)[o + 8] = p1;    // A2 = [w1 | w1]
+            (*out)[o + 12] = p1;
+            (*out)[o + 16] = p2;   // A3 = [w2 | w0]
+            (*out)[o + 20] = p0;
           }
 }
 
@@ -424,7 +431,8 @@ struct LayerRT {
   float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
   float* d_ww = nullptr;  // stride-1 layers: Winograd-packed U (conv3x3_wino.h)
   float* d_ww4 = nullptr; // 64 -> 64 stride-1 layers: F(4x4,3x3) U (conv3x3_wino4.h)
-  void* d_wbf = nullptr;  // stride-2 / transposed layers: bf16 parts of the weights (conv3x3_bf.h)
+  void* d_wbf[2] = {nullptr, nullptr};  // stride-2 / transposed layers: bf16 parts of the weights
+                                        // (conv3x3_bf.h), packed for NSPLIT 1 / 2
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
@@ -538,7 +546,8 @@ static int tkey(const tic_handle* h, const LayerRT& l, int n) {
   return f > 0 ? n + (f << 24) : n;
 }
 static const float* conv_weights(const LayerRT& l, const tic::ConvEntry* e) {
-  return e->wlds == 4 ? l.d_ww : (e->wlds == 5 ? l.d_ww4 : (e->wlds == 6 ? (const float*)l.d_wbf : l.d_w));
+  if (e->wlds == 6 || e->wlds == 7) return (const float*)l.d_wbf[e->nsplit == 2 ? 1 : 0];
+  return e->wlds == 4 ? l.d_ww : (e->wlds == 5 ? l.d_ww4 : l.d_w);
 }
 
 namespace {
@@ -1406,7 +1415,8 @@ void tic_destroy(tic_handle* h) {
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_ww4) (void)hipFree(l.d_ww4);
-    if (l.d_wbf) (void)hipFree(l.d_wbf);
+    for (void* p : l.d_wbf)
+      if (p) (void)hipFree(p);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
@@ -1509,15 +1519,20 @@ int tic_finalize(tic_handle* h) {
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_ww4) (void)hipFree(l.d_ww4);
-    if (l.d_wbf) (void)hipFree(l.d_wbf);
+    for (void*& p : l.d_wbf) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+    }
     if (l.d_b) (void)hipFree(l.d_b);
     l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_ww4 = l.d_b = nullptr;
-    l.d_wbf = nullptr;
     if (l.def.kind != K_S1 && i > 0 && i < L - 1 && l.def.cin % 16 == 0) {
-      std::vector<uint16_t> wb;
-      pack_bf(wp, l.def.cin, l.def.cout, &wb);
-      HIP_TRY(hipMalloc(&l.d_wbf, wb.size() * sizeof(uint16_t)));
-      HIP_TRY(hipMemcpy(l.d_wbf, wb.data(), wb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+      for (int ns = 1; ns <= 2; ++ns) {
+        if ((l.def.cout / ns) % 16) continue;
+        std::vector<uint16_t> wb;
+        pack_bf(wp, l.def.cin, l.def.cout, ns, &wb);
+        HIP_TRY(hipMalloc(&l.d_wbf[ns - 1], wb.size() * sizeof(uint16_t)));
+        HIP_TRY(hipMemcpy(l.d_wbf[ns - 1], wb.data(), wb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+      }
     }
     if (l.def.kind == K_S1 && i > 0 && i < L - 1) {
       std::vector<float> ww;
@@ -2364,9 +2379,9 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     if (e->wlds == 5)
       snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4, e->act,
                tf[e->res != 0], e->in, e->out);
-    else if (e->wlds == 6)
-      snprintf(buf, sizeof buf, "conv3x3_bf_kernel<%d,%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th,
-               e->wr, e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
+    else if (e->wlds == 6 || e->wlds == 7)
+      snprintf(buf, sizeof buf, "conv3x3_bf_kernel<%d,%d,%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th,
+               e->wr, e->nsplit, e->wlds - 6, e->act, tf[e->res != 0], e->in, e->out);
     else if (e->wlds == 4)
       snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
                e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
@@ -2505,9 +2520,9 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   if (e->wlds == 4) pack_wino(w_host, cin, cout, &wp);
   else if (e->wlds == 5) pack_wino4(w_host, cin, cout, &wp);
   else pack_generic(w_host, kind, cin, cout, &wp);
-  if (e->wlds == 6) {  // bf16 parts, 1.5x the bytes: carried in the f32 vector
+  if (e->wlds == 6 || e->wlds == 7) {  // bf16 parts (padded slabs): carried in the f32 vector
     std::vector<uint16_t> wb;
-    pack_bf(wp, cin, cout, &wb);
+    pack_bf(wp, cin, cout, e->nsplit, &wb);
     wp.assign((wb.size() + 1) / 2, 0.f);
     memcpy(wp.data(), wb.data(), wb.size() * sizeof(uint16_t));
   }
