@@ -1,7 +1,6 @@
 // conv_launch.h — grid computation + registry helpers for conv3x3_kernel instantiations.
 #pragma once
 #include "conv3x3.h"
-#include "conv3x3_bf.h"
 
 namespace tic {
 
@@ -11,15 +10,6 @@ static void launch_conv(const ConvArgs& a, int n, hipStream_t s) {
   const int wg = MODE == MODE_T2 ? a.W : a.Wo;
   dim3 grid(((wg + 15) / 16) * NSPLIT, (hg + TH - 1) / TH, n);
   hipLaunchKernelGGL((conv3x3_kernel<MODE, CIN, COUT, TH, WR, NSPLIT, WSRC, ACT, RES, IN, OUT>), grid, dim3(256), 0, s, a);
-}
-
-template <int MODE, int CIN, int COUT, int TH, int WR, int NSPLIT, int WSRC, int ACT, bool RES, int IN, int OUT>
-static void launch_conv_bf(const ConvArgs& a, int n, hipStream_t s) {
-  const int hg = MODE == MODE_T2 ? a.H : a.Ho;
-  const int wg = MODE == MODE_T2 ? a.W : a.Wo;
-  dim3 grid(((wg + 15) / 16) * NSPLIT, (hg + TH - 1) / TH, n);
-  hipLaunchKernelGGL((conv3x3_bf_kernel<MODE, CIN, COUT, TH, WR, NSPLIT, WSRC, ACT, RES, IN, OUT>), grid, dim3(256), 0,
-                     s, a);
 }
 
 }  // namespace tic
@@ -40,11 +30,3 @@ static void launch_conv_bf(const ConvArgs& a, int n, hipStream_t s) {
 #define TIC_CONV3(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT)           \
   TIC_CONV(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT),                  \
       TIC_CONVW(MODE, CIN, COUT, TH, WR, NSPLIT, 2, ACT, RES, IN, OUT)
-// f32 products on the bf16 matrix path (conv3x3_bf.h, its own weight packing): weight
-// source 6 = L2 into registers, 7 = LDS ring
-#define TIC_CONVBFW(MODE, CIN, COUT, TH, WR, NSPLIT, WSRC, ACT, RES, IN, OUT)      \
-  { MODE, CIN, COUT, ACT, RES, IN, OUT, TH, WR, NSPLIT, 6 + WSRC,                   \
-    &tic::launch_conv_bf<MODE, CIN, COUT, TH, WR, NSPLIT, WSRC, ACT, RES, IN, OUT> }
-#define TIC_CONVBF(MODE, CIN, COUT, TH, WR, NSPLIT, ACT, RES, IN, OUT)          \
-  TIC_CONVBFW(MODE, CIN, COUT, TH, WR, NSPLIT, 0, ACT, RES, IN, OUT),            \
-      TIC_CONVBFW(MODE, CIN, COUT, TH, WR, NSPLIT, 1, ACT, RES, IN, OUT)

@@ -24,17 +24,6 @@ static const ConvEntry kS2[] = {
     // base_model/ch_128 encode_2 (64 -> 128)
     TIC_CONVL2(MODE_S2, 64, 128, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONVL2(MODE_S2, 64, 128, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    // bf16x6 form (conv3x3_bf.h): model_0/3 encode_2, encode_3 / 64 -> 64, bottleneck (64 -> 80
-    // stays f32: its five channel blocks need TH 4, whose 64-channel stride-2 tile does not fit)
-    TIC_CONVBF(MODE_S2, 32, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_S2, 32, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_S2, 32, 64, 4, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBFW(MODE_S2, 64, 64, 2, 2, 1, 0, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_S2, 64, 64, 2, 2, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBFW(MODE_S2, 64, 64, 2, 1, 1, 0, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBFW(MODE_S2, 64, 64, 2, 2, 1, 0, ACT_ID, false, IN_F32, OUT_QUANT),
-    TIC_CONVBF(MODE_S2, 64, 64, 2, 2, 2, ACT_ID, false, IN_F32, OUT_QUANT),
-    TIC_CONVBFW(MODE_S2, 64, 64, 2, 1, 1, 0, ACT_ID, false, IN_F32, OUT_QUANT),
 };
 const ConvEntry* conv_registry_s2(int* count) {
   *count = sizeof(kS2) / sizeof(kS2[0]);

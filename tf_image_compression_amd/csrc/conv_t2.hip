@@ -26,20 +26,6 @@ static const ConvEntry kT2[] = {
     TIC_CONVL2(MODE_T2, 128, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONVL2(MODE_T2, 128, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
     TIC_CONVL2(MODE_T2, 128, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    // bf16x6 form (conv3x3_bf.h): decode_3 / decode_2 of model_0 and model_3
-    TIC_CONVBF(MODE_T2, 64, 64, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 2, 2, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 4, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 4, 4, 2, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 32, 2, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 32, 4, 4, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 32, 4, 2, 1, ACT_RELU, false, IN_F32, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 2, 2, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 2, 2, 2, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_CONVBF(MODE_T2, 64, 64, 4, 4, 2, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_CONVBF(MODE_T2, 80, 64, 2, 2, 1, ACT_ID, false, IN_IDX, OUT_F32),
-    TIC_CONVBFW(MODE_T2, 80, 64, 4, 4, 1, 0, ACT_ID, false, IN_IDX, OUT_F32),
 };
 const ConvEntry* conv_registry_t2(int* count) {
   *count = sizeof(kT2) / sizeof(kT2[0]);

@@ -87,11 +87,6 @@ struct Dec10Args {
   RgbOutArgs rgb;      // decode_0: wraw, bias, normalisation, outputs; rgb.H/W = 2H/2W
 };
 
-// conv3x3_bf.h weight slabs (shared with the host packing): row pitch in dwords of a (chunk,
-// lane group) row of cout_wg 12-dword channel records (three A tuples); = 0 mod 64 for cout_wg a
-// multiple of 16, which makes the ds_read_b128 of 16 channels x 4 lane groups conflict-free
-__host__ __device__ constexpr int bf_wpitch(int cout_wg) { return 12 * cout_wg; }
-
 typedef void (*ConvLaunch)(const ConvArgs&, int n, hipStream_t);
 
 struct ConvEntry {

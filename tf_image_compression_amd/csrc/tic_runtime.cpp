@@ -171,12 +171,9 @@ int same_pad(int kind, int h) {
 // workgroups.  `form` 1 selects the Winograd variants of stride-1 layers (weight source 4)
 // where compiled, 0 the direct ones.  TIC_FORCE_TILE="th,nsplit[,wsrc[,wr]]" overrides
 // (tuning experiments, tests); a forced weight source also overrides the form.
-// form of a compiled entry: 1 Winograd F(2x2,3x3) (weight source 4), 2 Winograd F(4x4,3x3)
-// (weight source 5), 3 the direct form with its f32 products on the bf16 matrix path
-// (conv3x3_bf.h, weight source 6), else 0 (direct, f32 MFMA)
-int entry_form(const tic::ConvEntry& c) {
-  return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : (c.wlds == 6 || c.wlds == 7 ? 3 : 0));
-}
+// stride-1 form of a compiled entry: 1 Winograd F(2x2,3x3) (weight source 4), 2 Winograd
+// F(4x4,3x3) (weight source 5), else 0 (direct)
+int entry_form(const tic::ConvEntry& c) { return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : 0); }
 
 // F(4x4,3x3) stages a patch through 32-bit buffer byte offsets: a patch (input or output) of
 // >= 2^29 floats cannot run in that form; every other entry fits any patch.
@@ -193,7 +190,7 @@ bool form_match(const tic::ConvEntry& c, int form, int fwl) {
 // instance runs F(2x2,3x3), one without Winograd instances the direct form.
 int form_fallback(int form, int pass) {
   if (pass == 0) return form;
-  if (pass == 1) return form == 2 ? 1 : (form == 1 || form == 3 ? 0 : -1);
+  if (pass == 1) return form == 2 ? 1 : (form == 1 ? 0 : -1);
   return form == 2 ? 0 : -1;
 }
 
@@ -274,49 +271,6 @@ void pack_generic(const float* k, int kind, int cin, int cout, std::vector<float
             const float v = kind == K_T2 ? k[((size_t)tap * cout + co) * cin + ci]   // [kh,kw,Cout,Cin]
                                          : k[((size_t)tap * cin + ci) * cout + co];  // HWIO
             (*wp)[((((size_t)tap * KC + kc) * 4 + g) * cout + co) * 4 + t] = v;
-          }
-}
-
-// bf16 parts of an f32 (round to nearest even), and back
-uint16_t bf16_rne(float f) {
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-float bf16_val(uint16_t h) {
-  const uint32_t u = (uint32_t)h << 16;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
-
-// conv3x3_bf.h weights from the generic packing (ci = 16 kc + 4 lg + t): per (tap, output-
-// channel split) a slab [Cin/16][4 lg][Cout/nsplit records of the three A tuples
-// [w0 | w0], [w1 | w1], [w2 | w0] (4 t each half, 24 bf16)], rows of tic::bf_wpitch dwords;
-// the parts w0 = rne(w), w1 = rne(w - w0), w2 = rne(w - w0 - w1) sum to w exactly
-void pack_bf(const std::vector<float>& wp, int cin, int cout, int nsplit, std::vector<uint16_t>* out) {
-  const int KC = cin / 16, cw = cout / nsplit, rp = tic::bf_wpitch(cw);  // rp in dwords
-  const size_t slab = (size_t)KC * 4 * rp * 2;                             // uint16 per slab
-  out->assign((size_t)9 * nsplit * slab, 0);
-  for (int tap = 0; tap < 9; ++tap)
-    for (int kc = 0; kc < KC; ++kc)
-      for (int g = 0; g < 4; ++g)
-        for (int co = 0; co < cout; ++co)
-          for (int t = 0; t < 4; ++t) {
-            const float w = wp[((((size_t)tap * KC + kc) * 4 + g) * cout + co) * 4 + t];
-            const uint16_t p0 = bf16_rne(w);
-            const float r = w - bf16_val(p0);
-            const uint16_t p1 = bf16_rne(r);
-            const uint16_t p2 = bf16_rne(r - bf16_val(p1));
-            const int sp = co / cw, cl = co % cw;
-            const size_t o = ((size_t)tap * nsplit + sp) * slab + ((size_t)kc * 4 + g) * rp * 2 + (size_t)cl * 24 + t;
-            (*out)[o] = p0;        // A1 = [w0 | w0]
-            (*out)[o + 4] = p0;
-            (*out)[o + 8] = p1;    // A2 = [w1 | w1]
-            (*out)[o + 12] = p1;
-            (*out)[o + 16] = p2;   // A3 = [w2 | w0]
-            (*out)[o + 20] = p0;
           }
 }
 
@@ -431,8 +385,6 @@ struct LayerRT {
   float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
   float* d_ww = nullptr;  // stride-1 layers: Winograd-packed U (conv3x3_wino.h)
   float* d_ww4 = nullptr; // 64 -> 64 stride-1 layers: F(4x4,3x3) U (conv3x3_wino4.h)
-  void* d_wbf[2] = {nullptr, nullptr};  // stride-2 / transposed layers: bf16 parts of the weights
-                                        // (conv3x3_bf.h), packed for NSPLIT 1 / 2
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
@@ -499,7 +451,6 @@ struct tic_handle {
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
   int wino4_max_n = 0;   // > 0: F(4x4,3x3) launches split into this many patches (tests of the split path)
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3), 2 F(4x4,3x3)
-  int mma = 0;           // stride-2 / transposed layers: 0 f32 MFMA, 1 f32 products on the bf16 path (form 3)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
@@ -538,15 +489,11 @@ static void touch(tic_handle* h) { h->stream_dirty = true; }
 
 // Key of a layer's tuned-tiling map: the batch size, per stride-1 form (each form has its
 // own candidate set, so switching the form never reuses the other form's choice).
-static int layer_form(const tic_handle* h, const LayerRT& l) {
-  return l.def.kind == K_S1 ? h->s1_form : (h->mma ? 3 : 0);
-}
 static int tkey(const tic_handle* h, const LayerRT& l, int n) {
-  const int f = layer_form(h, l);
-  return f > 0 ? n + (f << 24) : n;
+  return l.def.kind == K_S1 && h->s1_form > 0 ? n + (h->s1_form << 24) : n;
 }
+static int layer_form(const tic_handle* h, const LayerRT& l) { return l.def.kind == K_S1 ? h->s1_form : 0; }
 static const float* conv_weights(const LayerRT& l, const tic::ConvEntry* e) {
-  if (e->wlds == 6 || e->wlds == 7) return (const float*)l.d_wbf[e->nsplit == 2 ? 1 : 0];
   return e->wlds == 4 ? l.d_ww : (e->wlds == 5 ? l.d_ww4 : l.d_w);
 }
 
@@ -722,17 +669,6 @@ int default_s1_form(int model_id) {
   if (s == "wino") return 1;
   if (s == "direct") return 0;
   return model_id == 3 || model_id == TIC_MODEL_RMBE ? 2 : 1;
-}
-
-// f32-product policy of the stride-2 / transposed layers: TIC_MMA=bf16x6|f32, else built-in
-// (f32 until the bf16x6 form is measured faster for a model)
-int default_mma(int model_id) {
-  const char* f = getenv("TIC_MMA");
-  const std::string s = f ? f : "";
-  if (s == "bf16x6") return 1;
-  if (s == "f32") return 0;
-  (void)model_id;
-  return 0;
 }
 
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
@@ -1378,7 +1314,6 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
   h->s1_form = default_s1_form(model_id);
-  h->mma = default_mma(model_id);
   {
     const StructDefaults sd = struct_defaults(model_id);
     h->fuse01 = sd.fuse01;
@@ -1415,8 +1350,6 @@ void tic_destroy(tic_handle* h) {
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_ww4) (void)hipFree(l.d_ww4);
-    for (void* p : l.d_wbf)
-      if (p) (void)hipFree(p);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
@@ -1519,21 +1452,8 @@ int tic_finalize(tic_handle* h) {
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_ww4) (void)hipFree(l.d_ww4);
-    for (void*& p : l.d_wbf) {
-      if (p) (void)hipFree(p);
-      p = nullptr;
-    }
     if (l.d_b) (void)hipFree(l.d_b);
     l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_ww4 = l.d_b = nullptr;
-    if (l.def.kind != K_S1 && i > 0 && i < L - 1 && l.def.cin % 16 == 0) {
-      for (int ns = 1; ns <= 2; ++ns) {
-        if ((l.def.cout / ns) % 16) continue;
-        std::vector<uint16_t> wb;
-        pack_bf(wp, l.def.cin, l.def.cout, ns, &wb);
-        HIP_TRY(hipMalloc(&l.d_wbf[ns - 1], wb.size() * sizeof(uint16_t)));
-        HIP_TRY(hipMemcpy(l.d_wbf[ns - 1], wb.data(), wb.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-      }
-    }
     if (l.def.kind == K_S1 && i > 0 && i < L - 1) {
       std::vector<float> ww;
       pack_wino(l.k.data(), l.def.cin, l.def.cout, &ww);
@@ -1791,13 +1711,6 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->chain_order = value != 0;
-    return TIC_OK;
-  }
-  if (k == "mma") {  // stride-2 / transposed layers: 0 f32 MFMA, 1 bf16x6 (form 3), -1 the default
-    if (value < -1 || value > 1) return fail(TIC_EINVAL, "mma must be -1, 0 or 1");
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    clear_graphs(h);
-    h->mma = value < 0 ? default_mma(h->model_id) : value;
     return TIC_OK;
   }
   if (k == "s1_form") {  // 0 direct, 1 Winograd F(2,3), 2 F(4,3), -1 the default (TIC_S1_FORM or built-in)
@@ -2379,9 +2292,6 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
     if (e->wlds == 5)
       snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4, e->act,
                tf[e->res != 0], e->in, e->out);
-    else if (e->wlds == 6 || e->wlds == 7)
-      snprintf(buf, sizeof buf, "conv3x3_bf_kernel<%d,%d,%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->th,
-               e->wr, e->nsplit, e->wlds - 6, e->act, tf[e->res != 0], e->in, e->out);
     else if (e->wlds == 4)
       snprintf(buf, sizeof buf, "conv3x3_wino_kernel<%d,%d,%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 2, e->wr,
                e->nsplit, e->act, tf[e->res != 0], e->in, e->out);
@@ -2403,7 +2313,6 @@ int tic_tuning_export(const tic_handle* h, char* buf, int cap) {
   t += "flag fuse01 " + std::to_string((int)h->fuse01) + "\n";
   t += "flag fuse_tail " + std::to_string((int)h->fuse_tail) + "\n";
   t += "flag s1_form " + std::to_string(h->s1_form) + "\n";
-  t += "flag mma " + std::to_string(h->mma) + "\n";
   t += "flag chain " + std::to_string((int)h->chain) + "\n";
   t += "flag chain_wh " + std::to_string(h->chain_wh) + "\n";
   for (size_t i = 0; i < h->layers.size(); ++i) {
@@ -2429,7 +2338,6 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   std::vector<std::map<int, const tic::ConvEntry*>> tuned(L);
   std::vector<std::map<int, int>> vars(L);
   int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form, chain = h->chain, chain_wh = h->chain_wh;
-  int mma = h->mma;
   const char* p = text;
   int line = 0;
   while (*p) {
@@ -2449,7 +2357,6 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       if (!strcmp(name, "fuse01")) fuse01 = a != 0;
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
       else if (!strcmp(name, "s1_form") && a >= 0 && a <= 2) s1_form = a;
-      else if (!strcmp(name, "mma") && a >= 0 && a <= 1) mma = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
       else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 2) chain_wh = a;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
@@ -2497,7 +2404,6 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   h->fuse01 = fuse01;
   h->fuse_tail = fuse_tail;
   h->s1_form = s1_form;
-  h->mma = mma;
   h->chain = chain;
   h->chain_wh = chain_wh;
   return TIC_OK;
@@ -2512,7 +2418,7 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   HIP_TRY(hipSetDevice(h->device));
   const tic::ConvEntry* e = find_conv(kind, cin, cout, act, d_res ? 1 : 0, tic::IN_F32, tic::OUT_F32,
                                       kind == K_T2 ? H : out_size(kind, H), kind == K_T2 ? W : out_size(kind, W), n,
-                                      kind == K_S1 ? h->s1_form : (h->mma ? 3 : 0));
+                                      kind == K_S1 ? h->s1_form : 0);
   if (!e)
     return fail(TIC_EUNSUPPORTED, "no compiled conv3x3 for kind %d %d->%d act %d res %d", kind, cin, cout, act,
                 d_res ? 1 : 0);
@@ -2520,12 +2426,6 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   if (e->wlds == 4) pack_wino(w_host, cin, cout, &wp);
   else if (e->wlds == 5) pack_wino4(w_host, cin, cout, &wp);
   else pack_generic(w_host, kind, cin, cout, &wp);
-  if (e->wlds == 6 || e->wlds == 7) {  // bf16 parts (padded slabs): carried in the f32 vector
-    std::vector<uint16_t> wb;
-    pack_bf(wp, cin, cout, e->nsplit, &wb);
-    wp.assign((wb.size() + 1) / 2, 0.f);
-    memcpy(wp.data(), wb.data(), wb.size() * sizeof(uint16_t));
-  }
   Scratch s_w, s_b;
   HIP_TRY(s_w.alloc(wp.size() * 4));
   HIP_TRY(s_b.alloc((size_t)cout * 4));
