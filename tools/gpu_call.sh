@@ -9,7 +9,7 @@ CMD=$3
 for i in $(seq 1 20); do
   /usr/local/graft/bin/gpurun --timeout "$TMO" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if grep -q "status=transient\|status=refused.*already running" "$LOG" && ! grep -q "status=ok" "$LOG"; then
+  if grep -q "status=transient\|already running" "$LOG" && ! grep -q "status=ok" "$LOG"; then
     sleep 150
     continue
   fi
