@@ -144,3 +144,23 @@ def test_chain_cut_inside_res_block_fails_loudly(monkeypatch):
         monkeypatch.delenv("TIC_TEST_CHAIN_CUT")
         c.synchronize()
         assert np.array_equal(c.encode(x), ref)  # the handle stays usable
+
+
+@pytest.mark.parametrize("model_id,P,n", [(0, 256, 9), (3, 128, 3)])
+def test_wino_chain_region_orders_bit_identical(model_id, P, n):
+    """The chain's region orders (option chain_order: 0 atomic ticket, 1 blockIdx, 2 blockIdx
+    with a patch's regions on one XCD, -1 auto) only place the workgroups: the outputs are
+    identical (n = 9 at model_0: one full group of eight patches plus a tail patch that keeps
+    the identity order)."""
+    with _codec(model_id, P) as c:
+        x = structured_patches(n, P, seed=730 + model_id)
+        c.set_option("s1_form", 1)
+        c.set_option("chain", 1)
+        outs = []
+        for order in (0, 1, 2, -1):
+            c.set_option("chain_order", order)
+            for streams in (1, 2):
+                c.set_option("streams", streams)
+                outs.append(_run(c, x))
+        for got in outs[1:]:
+            assert all(np.array_equal(a, b) for a, b in zip(outs[0], got))

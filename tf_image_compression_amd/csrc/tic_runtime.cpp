@@ -454,7 +454,9 @@ struct tic_handle {
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
-  int chain_order = 0;     // 1: regions by blockIdx (dispatch order), 0: atomic ticket (option "chain_order")
+  int chain_order = -1;    // chain region order (option "chain_order"): 0 atomic ticket, 1 blockIdx,
+                           // 2 blockIdx XCD-aware, -1 auto: 2 when every lane's chain grid is
+                           // resident at once, else 0 (chain_launch_order)
   int mark_layer = -1;     // tic_mark_durations: time the launches starting at this layer
   // Lane scheduling: lanes join into `stream` after every call, but wait on it (fork) only
   // when something else was enqueued there since their last fork ("decouple"), so lane k's
@@ -764,6 +766,19 @@ static int chain_end(const tic_handle* h, int li) {
   while (j - li >= 2 && h->layers[j].def.residual) --j;
   return j - li >= 2 ? j : li;
 }
+// Region order of a chain launch of n patches x R regions (option "chain_order"; -1 = auto).
+// The hand-off protocol is placement-independent; placement only changes its speed: a
+// patch's R regions hand borders to each other every layer, and with the regions on one XCD
+// (order 2, wino_chain.h chain_region) model_0's step ran 3.0 % faster than with the atomic
+// ticket (profiles/ab_r05_chain_xcd.json).  Orders 1 and 2 take the region from blockIdx, so a
+// region may wait on one dispatched after it: that is only safe when every lane's chain grid
+// can be resident at once (then every workgroup gets a slot whatever the dispatch order);
+// otherwise the ticket (0), which never waits on a later ticket, is used.
+static int chain_launch_order(const tic_handle* h, int n, int R) {
+  if (h->chain_order >= 0) return h->chain_order;
+  const long slots = (long)h->num_cus * (h->chain_wh == 2 ? 1 : 2);
+  return (long)h->nlanes * n * R <= slots ? 2 : 0;
+}
 // layer i runs inside some wino_chain_kernel launch
 static bool in_chain(const tic_handle* h, int i) {
   for (int s = 1; s <= i; ++s)
@@ -936,7 +951,7 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       a.xbuf = ln.xbuf;
       a.flags = ln.cflags;
       a.ctl = ln.ctl;
-      a.dispatch_order = h->chain_order;
+      a.dispatch_order = chain_launch_order(h, n, R);
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
         int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R, st, &a.tstamp);
@@ -1324,7 +1339,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(2, std::max(1, atoi(f)));
-  if (const char* f = getenv("TIC_CHAIN_ORDER")) h->chain_order = atoi(f) != 0;
+  if (const char* f = getenv("TIC_CHAIN_ORDER")) h->chain_order = std::min(2, std::max(-1, atoi(f)));
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   for (int i = 0; i < 4 && e == hipSuccess; ++i) {
@@ -1707,10 +1722,11 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->chain_wh = value;
     return TIC_OK;
   }
-  if (k == "chain_order") {  // 1: chain regions by blockIdx (dispatch order), 0: atomic ticket
+  if (k == "chain_order") {  // 0 atomic ticket, 1 blockIdx, 2 blockIdx XCD-aware, -1 auto
+    if (value < -1 || value > 2) return fail(TIC_EINVAL, "chain_order must be -1, 0, 1 or 2");
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
-    h->chain_order = value != 0;
+    h->chain_order = value;
     return TIC_OK;
   }
   if (k == "s1_form") {  // 0 direct, 1 Winograd F(2,3), 2 F(4,3), -1 the default (TIC_S1_FORM or built-in)

@@ -61,7 +61,8 @@ struct ChainArgs {
   unsigned* flags;      // [nl-1][n*R] epoch flags
   unsigned* ctl;        // [0] ticket, [1] done count, [2] epoch, [3] error (poll timeout)
   int dispatch_order;   // 1: a workgroup's region is its blockIdx.x (the hardware's in-order
-                        // dispatch); 0: an atomic ticket (order guaranteed whatever the dispatch)
+                        // dispatch); 2: the same, XCD-aware (chain_region); 0: an atomic ticket
+                        // (order guaranteed whatever the dispatch)
   int probe;            // timing probes only (TIC_CHAIN_PROBE; results invalid unless 0):
                         // 1 = no hand-off at all, 2 = publish but do not wait / read
   unsigned long long* tstamp;  // phase timestamps (TIC_CHAIN_TIMING; results stay valid) or
@@ -80,6 +81,18 @@ constexpr unsigned kSpinLimit = 1u << 19;  // ~0.5 s of polling before the error
 
 // LDS float offset of staged pixel (row, col) of a 10x10 tile (columns split by parity)
 __device__ __forceinline__ int tpix(int row, int col) { return (row * RP + (col & 1) * HP + (col >> 1)) * PS; }
+
+// Dispatch order 2: blocks b and b + 8 are dealt to one XCD (MI355X_MICROARCH.md), so block b
+// of a group of 8 R blocks takes region r of patch (group * 8 + b % 8) with r = (b / 8) % R:
+// the R regions of a patch, which hand their borders to each other every layer, run on ONE
+// XCD and meet in its L2 instead of crossing the fabric.  A bijection on [0, n R): the last
+// n % 8 patches keep the identity.
+__device__ __forceinline__ unsigned chain_region(unsigned b, unsigned R, unsigned n) {
+  const unsigned full = (n / 8) * 8 * R;
+  if (b >= full) return b;
+  const unsigned x = b & 7u, s = b >> 3;
+  return ((s / R) * 8 + x) * R + s % R;
+}
 
 // 16-byte write-through (sc1) store / sc1 load through a buffer resource (aux 16 = sc1):
 // one buffer_store/load_dwordx4 instead of two 8-byte atomics (MI355X_MICROARCH.md: 8-B
@@ -126,7 +139,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   stamp(0);
 
   if (tid == 0) {
-    sh[0] = a.dispatch_order ? blockIdx.x : __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[0] = a.dispatch_order == 2   ? chain_region(blockIdx.x, (unsigned)(a.rh * a.rw), (unsigned)a.n)
+            : a.dispatch_order == 1 ? blockIdx.x
+                                    : __hip_atomic_fetch_add(&a.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh[1] = __hip_atomic_load(&a.ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // every layer's bias, read by the epilogues from LDS
