@@ -129,7 +129,10 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
         launch = []
         for k in kernels:
             launch.append(k if k or not launch else launch[-1])
-        work = [(lay, f * wino_frac(launch[i]), b, ho) for i, (lay, f, b, ho) in enumerate(work)]
+        # (Winograd forms run stride-1 layers only: a chain launch's stride-2 head / transposed
+        # tail is direct)
+        work = [(lay, f * (wino_frac(launch[i]) if lay.kind in ("conv_s1", "res") else 1.0), b, ho)
+                for i, (lay, f, b, ho) in enumerate(work)]
 
     def out_res_bytes(i):
         lay, _, _, ho = work[i]

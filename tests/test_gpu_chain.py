@@ -7,6 +7,8 @@ and at patch sizes whose bottleneck is a single partial region (P = 48, 64), 2x2
 batches whose grid exceeds what the GPU holds at once (the ticket order must keep every
 patch's regions co-resident).  Reference layers: model_0/model.py:98-196,
 model_3/model.py:66-281, submit/2/rmbe/model.py:140-160."""
+import re
+
 import numpy as np
 import pytest
 
@@ -37,11 +39,12 @@ def test_wino_chain_bit_identical(model_id, P, n):
         ref = _run(c, x)
         assert not any("wino_chain" in k for k in c.layer_kernels(n))
         c.set_option("chain", 1)
+        c.set_option("chain_x", 0)
         for wh in (1, 2):  # 256- / 512-thread workgroups
             c.set_option("chain_wh", wh)
             c.set_option("streams", 1)
             kern = c.layer_kernels(n)
-            assert any(k.startswith("wino_chain_kernel") and k.endswith(f",{wh}>") for k in kern), kern
+            assert any(re.fullmatch(rf"wino_chain_kernel<\d,\d,{wh},\d>", k) for k in kern), kern
             got = _run(c, x)
             for a, b in zip(ref, got):
                 assert np.array_equal(a, b)
@@ -164,3 +167,57 @@ def test_wino_chain_region_orders_bit_identical(model_id, P, n):
                 outs.append(_run(c, x))
         for got in outs[1:]:
             assert all(np.array_equal(a, b) for a, b in zip(outs[0], got))
+
+
+@pytest.mark.parametrize("model_id,P,n", [(0, 256, 6), (0, 64, 5), (0, 48, 3), (1, 64, 4), (2, 128, 3)])
+def test_wino_chain_stride2_neighbours_bit_identical(model_id, P, n):
+    """Option chain_x: the encoder's stride-2 layer in front of a run (encode_3) as the chain
+    launch's head and the decoder's transposed layer behind it (decode_3) as its tail
+    (wino_chain.h HT).  They replay conv3x3_kernel's MODE_S2 / MODE_T2 step order, so the
+    whole codec stays bit-identical to the unfused launches: at 2x2 regions (model_0 at 256,
+    model_2 at 128), a single region with its halo outside the image (P = 64) and a single
+    partial region (P = 48), one lane and two.  Reference layers: model_0/model.py:90-96
+    (encode_3), 198-206 (decode_3); model_2/model.py."""
+    with _codec(model_id, P) as c:
+        x = structured_patches(n, P, seed=740 + model_id + P)
+        c.set_option("s1_form", 1)
+        c.set_option("chain", 0)
+        ref = _run(c, x)
+        c.set_option("chain", 1)
+        c.set_option("chain_wh", 2)
+        c.set_option("chain_x", 1)
+        for streams in (1, 2):
+            c.set_option("streams", streams)
+            kern = c.layer_kernels(n)
+            heads = [k for k in kern if re.fullmatch(r"wino_chain_kernel<\d,\d,2,[13]>", k)]
+            tails = [k for k in kern if re.fullmatch(r"wino_chain_kernel<\d,\d,2,[23]>", k)]
+            assert heads and tails, kern
+            # the head's launch starts at encode_3 and carries the run; decode_3 has no launch
+            names = [lay[0] for lay in c.layers()]
+            assert kern[names.index("encode_3")] in heads and kern[names.index("encode_3") + 1] == "", kern
+            assert kern[names.index("decode_3")] == "", kern
+            got = _run(c, x)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b)
+        c.set_option("chain_x", 0)
+        assert not any(re.fullmatch(r"wino_chain_kernel<\d,\d,2,[123]>", k) for k in c.layer_kernels(n))
+
+
+def test_wino_chain_stride2_neighbours_oversubscribed():
+    """The head / tail launches with 2 x 256 patches (2048 region workgroups, more than are
+    resident): the ticket order still completes them, epoch after epoch."""
+    with _codec(0, 256) as c:
+        x = structured_patches(8, 256, seed=760)
+        big = np.concatenate([x] * 64)
+        c.set_option("chain", 0)
+        ref_idx = c.encode(x)
+        ref_u8 = c.decode(ref_idx)
+        c.set_option("chain", 1)
+        c.set_option("chain_wh", 2)
+        c.set_option("chain_x", 1)
+        c.set_option("chunk", 512)
+        for _ in range(3):
+            idx = c.encode(big)
+            assert all(np.array_equal(idx[i * 8:(i + 1) * 8], ref_idx) for i in range(64))
+        u8 = c.decode(idx)
+        assert all(np.array_equal(u8[i * 8:(i + 1) * 8], ref_u8) for i in range(64))

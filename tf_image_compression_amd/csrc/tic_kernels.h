@@ -126,7 +126,7 @@ bool launch_dec10(int c1, int c0, const Dec10Args& a, int n, hipStream_t s, int 
 struct ChainArgs;
 // wh: 1 = 256-thread workgroups, 2 = 512-thread workgroups (output channels split in halves
 // over the waves)
-bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh);
+bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_t s, int wh, int ht = 0);
 
 // Whole-image glue and the symbol histogram (image_ops.hip).
 void launch_tile_reflect(const uint8_t* img, int H, int W, int P, int hn, int wn, uint8_t* out, int num_cus,

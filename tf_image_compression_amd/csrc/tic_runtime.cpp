@@ -454,6 +454,9 @@ struct tic_handle {
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
+  bool chain_x = false;    // the stride-2 neighbours of a run inside its launch (option "chain_x":
+                           // the encoder's stride-2 layer in front as the head, the decoder's
+                           // transposed layer behind as the tail; wino_chain.h HT)
   int chain_order = -1;    // chain region order (option "chain_order"): 0 atomic ticket, 1 blockIdx,
                            // 2 blockIdx XCD-aware, -1 auto: 2 when every lane's chain grid is
                            // resident at once, else 0 (chain_launch_order)
@@ -653,11 +656,11 @@ const int kRgbInDefault = 2;   // TH 16
 // stages (model_0/1/2: measured faster) but not for model_3's 64x64 / 32x32 stages or the
 // rmbe net (the step tuner keeps it off there).
 struct StructDefaults {
-  bool fuse01, fuse_tail, chain;
+  bool fuse01, fuse_tail, chain, chain_x;
 };
 StructDefaults struct_defaults(int model_id) {
   const bool small_stages = model_id == 0 || model_id == 1 || model_id == 2;
-  return {true, true, small_stages};
+  return {true, true, small_stages, false};
 }
 
 // Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino|wino4, else built-in:
@@ -779,15 +782,71 @@ static int chain_launch_order(const tic_handle* h, int n, int R) {
   const long slots = (long)h->num_cus * (h->chain_wh == 2 ? 1 : 2);
   return (long)h->nlanes * n * R <= slots ? 2 : 0;
 }
+// One wino_chain_kernel launch: the stride-1 run [s1, end) and, with the option "chain_x",
+// the encoder's stride-2 64->64 ReLU layer right in front of it as the head (start = s1 - 1;
+// only in front of a run that starts a res_block, whose block input the head writes) and the
+// decoder's transposed 64->64 ReLU layer right behind it as the tail (layer `end`).  Both need
+// the 512-thread workgroup and every region of the launch resident at once (margin 2x): they
+// add a hand-off, and the per-lane grid must not depend on the dispatch order's residency
+// argument for more than the run's own layers.
+struct ChainSpan {
+  int start = -1, s1 = -1, end = -1;
+  bool head = false, tail = false;
+  int last() const { return end - 1 + (tail ? 1 : 0); }
+  bool valid() const { return start >= 0; }
+};
+static bool s2_64_relu(const LayerDef& d, int kind) {
+  return d.kind == kind && d.cin == 64 && d.cout == 64 && d.act == 1 && !d.residual;
+}
+static bool chain_x_fits(const tic_handle* h, int hw) {
+  const long rw = (hw + 7) / 8;
+  return h->chain_x && h->chain_wh == 2 && 2L * h->nlanes * rw * rw <= (long)h->num_cus;
+}
+// the launch that starts at layer li (invalid if none does)
+static ChainSpan chain_span_at(const tic_handle* h, int li) {
+  ChainSpan sp;
+  const int L = (int)h->layers.size();
+  int s1 = li;
+  bool head = false;
+  if (h->chain_x && li >= 1 && li + 2 < L && s2_64_relu(h->layers[li].def, K_S2) && !(li <= 1 && fuses01(h)) &&
+      chain_end(h, li + 1) > li + 2 && h->layers[li + 2].def.residual && chain_x_fits(h, h->layers[li + 1].h_in)) {
+    head = true;
+    s1 = li + 1;
+  }
+  const int ce = chain_end(h, s1);
+  if (ce <= s1) return sp;
+  sp.start = li;
+  sp.s1 = s1;
+  sp.end = ce;
+  sp.head = head;
+  sp.tail = ce < L - 1 && s2_64_relu(h->layers[ce].def, K_T2) && !(ce >= L - 2 && fuses_tail(h)) &&
+            (h->rmbe() || ce > h->n_enc) && h->layers[ce].h_in == h->layers[s1].h_in &&
+            chain_x_fits(h, h->layers[s1].h_in);
+  return sp;
+}
+// every chain launch of the network, in order (as run_layers walks it)
+static std::vector<ChainSpan> chain_spans(const tic_handle* h) {
+  std::vector<ChainSpan> v;
+  const int L = (int)h->layers.size();
+  for (int i = 1; i < L - 1; ++i) {
+    const ChainSpan sp = chain_span_at(h, i);
+    if (!sp.valid()) continue;
+    v.push_back(sp);
+    i = sp.last();
+  }
+  return v;
+}
 // layer i runs inside some wino_chain_kernel launch
 static bool in_chain(const tic_handle* h, int i) {
-  for (int s = 1; s <= i; ++s)
-    if (chain_end(h, s) > i) return true;  // a chain starting at s covers s..chain_end-1
+  for (const ChainSpan& sp : chain_spans(h))
+    if (sp.start <= i && i <= sp.last()) return true;
   return false;
 }
-static bool any_chain(const tic_handle* h) {
-  for (int i = 0; i < (int)h->layers.size(); ++i)
-    if (chain_end(h, i) > i) return true;
+static bool any_chain(const tic_handle* h) { return !chain_spans(h).empty(); }
+// whether the option "chain_x" changes the launch plan at all
+static bool any_chain_x(const tic_handle* h) {
+  for (const ChainSpan& sp : chain_spans(h))
+    if (sp.head || sp.tail) return true;
   return false;
 }
 
@@ -927,51 +986,65 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
       }
       break;
     }
-    const int ce = chain_end(h, li);
-    if (ce > li && ce <= l1) {
-      const int nl = ce - li;
+    const ChainSpan sp = chain_span_at(h, li);
+    if (sp.valid() && sp.last() < l1) {
+      const int s1 = sp.s1, ce = sp.end, nl = ce - s1;
+      const LayerRT& lr = h->layers[s1];  // the run's first stride-1 layer
+      const bool first_dec_c = !h->rmbe() && s1 == h->n_enc;
       const bool last_enc_c = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      const int R = ((lay.h_in + 7) / 8) * ((lay.h_in + 7) / 8);  // 8x8 regions per patch
-      int rc = ensure_chain(h, ln, nl, n, R);
+      const int R = ((lr.h_in + 7) / 8) * ((lr.h_in + 7) / 8);  // 8x8 regions per patch
+      int rc = ensure_chain(h, ln, nl + (sp.head ? 1 : 0) + (sp.tail ? 1 : 0), n, R);  // hand-offs + 1
       if (rc) return rc;
       tic::ChainArgs a{};
       for (int k = 0; k < nl; ++k) {
-        const LayerRT& lk = h->layers[li + k];
+        const LayerRT& lk = h->layers[s1 + k];
         a.layer[k] = {lk.d_ww, lk.d_b, lk.def.act, lk.def.residual};
       }
       a.nl = nl;
-      a.in = first_dec ? in : (const void*)src;
+      a.in = first_dec_c ? in : (const void*)src;
       a.lut = h->d_lut;
       a.out = last_enc_c ? d_pre : ws[dst];
       a.qout = last_enc_c ? d_idx : nullptr;
       a.qscale = (float)(h->Q - 1);
-      a.H = a.W = lay.h_in;
-      a.rh = a.rw = (lay.h_in + 7) / 8;
+      a.H = a.W = lr.h_in;
+      a.rh = a.rw = (lr.h_in + 7) / 8;
       a.n = n;
       a.xbuf = ln.xbuf;
       a.flags = ln.cflags;
       a.ctl = ln.ctl;
       a.dispatch_order = chain_launch_order(h, n, R);
+      if (sp.head) {  // the stride-2 layer in front (layer li): its direct packing, input = src
+        a.head = {lay.d_w, lay.d_b, d.act, 0};
+        a.head_in = src;
+        a.hH = a.hW = lay.h_in;
+        a.hpad = same_pad(K_S2, lay.h_in);
+      }
+      if (sp.tail) {  // the transposed layer behind (layer ce), writing the next activation
+        const LayerRT& tl = h->layers[ce];
+        a.tail = {tl.d_w, tl.d_b, tl.def.act, 0};
+        a.tail_out = ws[dst];
+      }
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
-        int rc2 = probe_stamps(ln, first_dec ? 1 : 0, n * R, st, &a.tstamp);
+        int rc2 = probe_stamps(ln, first_dec_c || sp.tail ? 1 : 0, n * R, st, &a.tstamp);
         if (rc2) return rc2;
       }
-      const int inm = first_dec ? tic::IN_IDX : tic::IN_F32, outm = last_enc_c ? tic::OUT_QUANT : tic::OUT_F32;
-      if (!tic::launch_wino_chain(inm, outm, a, st, h->chain_wh))
-        return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, ce - 1);
+      const int inm = first_dec_c ? tic::IN_IDX : tic::IN_F32, outm = last_enc_c ? tic::OUT_QUANT : tic::OUT_F32;
+      const int ht = (sp.head ? tic::CH_HEAD : 0) | (sp.tail ? tic::CH_TAIL : 0);
+      if (!tic::launch_wino_chain(inm, outm, a, st, h->chain_wh, ht))
+        return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, sp.last());
       rc = check_launch();
       if (rc) return rc;
       if (prof.ev) {
         HIP_TRY(hipEventRecord(prof.ev[2 * li + 1], st));
-        for (int k = li + 1; k < ce; ++k) {  // the other layers ran inside this launch
+        for (int k = li + 1; k <= sp.last(); ++k) {  // the other layers ran inside this launch
           HIP_TRY(hipEventRecord(prof.ev[2 * k], st));
           HIP_TRY(hipEventRecord(prof.ev[2 * k + 1], st));
         }
       }
       block_in = -1;
       cur = dst;
-      li = ce - 1;
+      li = sp.last();
       continue;
     }
     if (first) {
@@ -1334,11 +1407,13 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
     h->fuse01 = sd.fuse01;
     h->fuse_tail = sd.fuse_tail;
     h->chain = sd.chain;
+    h->chain_x = sd.chain_x;
   }
   if (const char* f = getenv("TIC_FUSE01")) h->fuse01 = atoi(f) != 0;
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(2, std::max(1, atoi(f)));
+  if (const char* f = getenv("TIC_CHAIN_X")) h->chain_x = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN_ORDER")) h->chain_order = std::min(2, std::max(-1, atoi(f)));
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -1720,6 +1795,13 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->chain_wh = value;
+    return TIC_OK;
+  }
+  if (k == "chain_x") {  // the stride-2 neighbours of a run in its launch (head / tail)
+    if (value < -1 || value > 1) return fail(TIC_EINVAL, "chain_x must be -1, 0 or 1");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->chain_x = value < 0 ? struct_defaults(h->model_id).chain_x : value != 0;
     return TIC_OK;
   }
   if (k == "chain_order") {  // 0 atomic ticket, 1 blockIdx, 2 blockIdx XCD-aware, -1 auto
@@ -2108,6 +2190,15 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     if (fits) rc = confirm([&](bool alt) { h->chain_wh = alt ? other : was; }, 0.005f, "chain_wh", &keep, &cur);
     clear_graphs(h);
   }
+  if (!rc && h->chain && !getenv("TIC_CHAIN_X")) {  // the stride-2 neighbours inside the chain's launch
+    const bool was = h->chain_x;
+    h->chain_x = true;
+    const bool can = any_chain_x(h);
+    h->chain_x = was;
+    bool keep = false;
+    if (can) rc = confirm([&](bool alt) { h->chain_x = alt ? !was : was; }, 0.005f, "chain_x", &keep, &cur);
+    clear_graphs(h);
+  }
   const int L = (int)h->layers.size();
   for (int round = 0; round < rounds && !rc; ++round) {
     for (int i = 0; i < L && !rc; ++i) {
@@ -2257,14 +2348,15 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   const int L = (int)h->layers.size();
   const char* tf[2] = {"false", "true"};
   char buf[160] = "";
-  int cs = -1;  // start of the chain containing layer i
-  for (int s0 = 1; s0 <= i; ++s0)
-    if (chain_end(h, s0) > i && chain_end(h, s0) > s0) cs = s0;
-  if (cs >= 0) {
-    if (cs == i) {
-      const int ce = chain_end(h, cs);
-      const bool first_dec = !h->rmbe() && cs == h->n_enc, last_enc = !h->rmbe() && ce - 1 == h->n_enc - 1;
-      snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh);
+  ChainSpan cs;  // the chain launch containing layer i
+  for (const ChainSpan& sp : chain_spans(h))
+    if (sp.start <= i && i <= sp.last()) cs = sp;
+  if (cs.valid()) {
+    if (cs.start == i) {
+      const bool first_dec = !h->rmbe() && cs.s1 == h->n_enc, last_enc = !h->rmbe() && cs.end - 1 == h->n_enc - 1;
+      const int ht = (cs.head ? tic::CH_HEAD : 0) | (cs.tail ? tic::CH_TAIL : 0);
+      snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh,
+               ht);
     }
   } else if (fuses_tail(h) && i >= L - 2) {
     if (i == L - 2) {
@@ -2331,6 +2423,7 @@ int tic_tuning_export(const tic_handle* h, char* buf, int cap) {
   t += "flag s1_form " + std::to_string(h->s1_form) + "\n";
   t += "flag chain " + std::to_string((int)h->chain) + "\n";
   t += "flag chain_wh " + std::to_string(h->chain_wh) + "\n";
+  t += "flag chain_x " + std::to_string((int)h->chain_x) + "\n";
   for (size_t i = 0; i < h->layers.size(); ++i) {
     const LayerRT& l = h->layers[i];
     for (const auto& kv : l.tuned) {
@@ -2354,6 +2447,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   std::vector<std::map<int, const tic::ConvEntry*>> tuned(L);
   std::vector<std::map<int, int>> vars(L);
   int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form, chain = h->chain, chain_wh = h->chain_wh;
+  int chain_x = h->chain_x;
   const char* p = text;
   int line = 0;
   while (*p) {
@@ -2375,6 +2469,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       else if (!strcmp(name, "s1_form") && a >= 0 && a <= 2) s1_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
       else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 2) chain_wh = a;
+      else if (!strcmp(name, "chain_x")) chain_x = a != 0;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
     } else if (!strcmp(kind, "conv")) {
       if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)
@@ -2422,6 +2517,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   h->s1_form = s1_form;
   h->chain = chain;
   h->chain_wh = chain_wh;
+  h->chain_x = chain_x;
   return TIC_OK;
 }
 

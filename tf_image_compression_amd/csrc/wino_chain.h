@@ -29,6 +29,17 @@
 // without waiting on it.  Every poll is bounded as well (error flag, never a hang).
 // The last workgroup to finish resets the ticket and advances the launch epoch that the
 // flags are compared against, so no buffer needs clearing between launches.
+//
+// Stride-2 neighbours (HT, round 5): the encoder's stride-2 layer in front of the run
+// (model_0/1/2 encode_3, model_0/model.py:90-96) can run as the chain's HEAD, and the
+// decoder's transposed layer behind it (decode_3, :198-206) as its TAIL, in the same
+// launch.  The head stages the 17x17 input window of its 8x8 output region (columns split by
+// parity, so the 8 outputs of a row read consecutive LDS pixels), runs conv3x3_kernel<
+// MODE_S2>'s implicit GEMM in its exact step order (tap-major, 16-channel chunk, t), and
+// hands its output border over like a chain layer; the tail runs conv3x3_kernel<MODE_T2>'s
+// four sub-pixel phases from the run's last tile (halo from one more hand-off) and writes
+// the 16x16 output tile of its region.  Both are bit-identical to the standalone launches
+// (tests/test_gpu_chain.py); they remove two launches per lane and their HBM round trips.
 #pragma once
 #include "conv3x3_wino.h"
 
@@ -36,8 +47,12 @@ namespace tic {
 
 constexpr int CH_MAX_LAYERS = 8;
 // timestamps per workgroup: kernel start, input staged, then per layer: start, K loop done,
-// epilogue done, border published, neighbours' flags seen, halo staged
-constexpr int CH_TS = 2 + 6 * CH_MAX_LAYERS;
+// epilogue done, border published, neighbours' flags seen, halo staged; then the head's six
+// (window staged, K loop done, epilogue done, published, flags seen, halo staged) and the
+// tail's (start, K loop done, stores issued)
+constexpr int CH_TS = 2 + 6 * (CH_MAX_LAYERS + 2);
+constexpr int CH_HEAD_TS = 2 + 6 * CH_MAX_LAYERS, CH_TAIL_TS = CH_HEAD_TS + 6;
+constexpr int CH_HEAD = 1, CH_TAIL = 2;  // HT bits
 
 struct ChainLayer {
   const float* wu;    // Winograd U [16 p][4 kc][4 g][64][4 t] (pack_wino)
@@ -67,6 +82,17 @@ struct ChainArgs {
                         // 1 = no hand-off at all, 2 = publish but do not wait / read
   unsigned long long* tstamp;  // phase timestamps (TIC_CHAIN_TIMING; results stay valid) or
                                // null: [workgroup][CH_TS] s_memrealtime (100 MHz) by thread 0
+  // HT & CH_HEAD: the stride-2 64->64 layer in front of the run.  head.wu = its direct
+  // packing [9 tap][4 kc][4 g][64][4 t] (pack_generic); head_in f32 [n, hH, hW, 64], TF SAME
+  // pad_before hpad; its output (H x W) is the run's first input (the block input).
+  ChainLayer head;
+  const float* head_in;
+  int hH, hW, hpad;
+  // HT & CH_TAIL: the stride-2 transposed 64->64 layer behind the run (direct packing of the
+  // [3,3,Cout,Cin] kernel); the run's last output stays in LDS, the tail writes f32
+  // [n, 2H, 2W, 64] to tail_out.
+  ChainLayer tail;
+  float* tail_out;
 };
 
 namespace chain {
@@ -117,15 +143,22 @@ __device__ __forceinline__ f32x4 ld_sc1_16(__amdgpu_buffer_rsrc_t r, int byte_of
 // output channels of points (xi, 0..3); 2: a 512-thread workgroup, waves xi and xi + 4
 // split the output channels in halves (two waves per SIMD hide each other's LDS / L2
 // latency; every output's fma order is unchanged, so both are bit-identical).
-template <int IN, int OUT, int WH = 1>
+template <int IN, int OUT, int WH = 1, int HT = 0>
 __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(const ChainArgs a) {
   using namespace chain;
   constexpr int NTH = 256 * WH;
+  constexpr bool HEAD = (HT & CH_HEAD) != 0, TAIL = (HT & CH_TAIL) != 0;
+  static_assert(HT == 0 || WH == 2, "stride-2 head / tail: 512-thread workgroups only");
   // WH = 2 (one workgroup per CU): the T exchange gets a buffer of its own beside the two
   // tiles, so it never aliases a tile and needs no barrier of its own
   constexpr bool SEPX = WH == 2;
   constexpr int TSTR = SEPX ? TILE : TB;
-  __shared__ __attribute__((aligned(16))) float smem[SEPX ? 2 * TILE + XCH : 2 * TB];
+  // the head's input window: 17 rows x (9 even + 8 odd columns + 1 pad) pixels, after tile A
+  // (the block input the head writes); it aliases tile B, the exchange and what follows
+  constexpr int HWR = 17, HWC = 18, HWIN = HWR * HWC * PS;
+  constexpr int SM0 = SEPX ? 2 * TILE + XCH : 2 * TB;
+  constexpr int SMEM = HEAD && TILE + HWIN > SM0 ? TILE + HWIN : SM0;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   __shared__ __attribute__((aligned(16))) float sbias[CH_MAX_LAYERS * C];
   __shared__ unsigned sh[2];
   const int tid = threadIdx.x;
@@ -152,6 +185,8 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   const int nimg = ticket / R, reg = ticket % R;
   const int ry = reg / a.rw, rx = reg % a.rw;
   const int oy0 = ry * 8, ox0 = rx * 8;
+  const size_t g = (size_t)nimg * R + reg;
+  constexpr int KH = HEAD ? 1 : 0;  // hand-off slot of chain layer l: KH + l
 
   // ---- weights of layer l, step s = 4 kc + nu, straight from L2, prefetched PF ahead:
   // raw buffer loads — the layer's descriptor in SGPRs, this lane's byte offset in one VGPR
@@ -171,20 +206,221 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         __builtin_amdgcn_raw_buffer_load_b128(r, wlane, ((nu * KC + kc) * 16 * C + (wh * NBW + nb) * 64) * 4, 0);
     return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
   };
-  {
-    const __amdgpu_buffer_rsrc_t w0 = wsrc(0);
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-#pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(w0, p, nb);
-  }
 
-  // ---- stage the first layer's input tile (zero outside the image = SAME padding) ----
   // The first layer's tile is the res_block input when the chain starts a block, so it
-  // goes to tile 0 (A) then, else to tile 1 (B): the block input always lives in A.
+  // goes to tile 0 (A) then, else to tile 1 (B): the block input always lives in A.  (A head
+  // is only planned in front of a block: its output is the block input, tile A.)
   const bool first_block = a.nl > 1 && a.layer[1].res;
-  float* src = first_block ? smem : smem + TSTR;
-  {
+  float* src = HEAD || first_block ? smem : smem + TSTR;
+
+  bool failed = false;
+  // halo descriptors of this thread, the same for every hand-off: the LDS offset in the tile
+  // and the byte offset of the neighbour's border record entry inside a hand-off buffer
+  // (-1: outside the image, zero)
+  constexpr int HK = (36 * 16 + NTH - 1) / NTH;
+  int hlds[HK], hsrc[HK];
+#pragma unroll
+  for (int k = 0; k < HK; ++k) {
+    const int e = k * NTH + tid;
+    hlds[k] = hsrc[k] = -1;
+    if (e < 36 * 16) {
+      const int hp = e >> 4, q = e & 15;
+      int hy, hx;
+      if (hp < 10) hy = -1, hx = hp - 1;
+      else if (hp < 20) hy = 8, hx = hp - 11;
+      else if (hp < 28) hy = hp - 20, hx = -1;
+      else hy = hp - 28, hx = 8;
+      hlds[k] = tpix(hy + 1, hx + 1) + 4 * q;
+      const int gy = oy0 + hy, gx = ox0 + hx;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
+        const int ny = hy & 7, nx = hx & 7;  // pixel inside the neighbour region
+        int side, idx;
+        if (hy < 0) side = 1, idx = nx;
+        else if (hy > 7) side = 0, idx = nx;
+        else if (hx < 0) side = 3, idx = ny;
+        else side = 2, idx = ny;
+        const int gn = nimg * R + nry * a.rw + nrx;
+        hsrc[k] = (gn * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q) * 4;
+      }
+    }
+  }
+  const bool handoff_on = R > 1 && a.probe != 1;
+  // this region's border record of hand-off k
+  auto pub_rsrc = [&](int k) { return xrsrc(a.xbuf + ((size_t)k * nR + g) * (4 * 8 * C), 4 * 8 * C * 4); };
+  // publish pixel (ly, lx) of the region's output (16-byte write-through stores into the 8 KB
+  // record: side 0 / 1 = rows 0 / 7, side 2 / 3 = columns 0 / 7; corners go to two sides)
+  auto publish = [&](const __amdgpu_buffer_rsrc_t& rpub, int ly, int lx, int co, f32x4 v) {
+    if (ly == 0) st_sc1_16(rpub, ((0 * 8 + lx) * C + co) * 4, v);
+    if (ly == 7) st_sc1_16(rpub, ((1 * 8 + lx) * C + co) * 4, v);
+    if (lx == 0) st_sc1_16(rpub, ((2 * 8 + ly) * C + co) * 4, v);
+    if (lx == 7) st_sc1_16(rpub, ((3 * 8 + ly) * C + co) * 4, v);
+  };
+  // hand-off k: (every storing thread drained its border stores and passed a barrier) raise
+  // this region's flag, wait for the (up to 8) neighbours' flags, read the halo ring of `tile`
+  // (rows 0 and 9, columns 0 and 9: 36 px x 16 quads) through the descriptors above
+  auto handoff = [&](int k, float* tile, int ts) {
+    if (handoff_on) {
+      if (tid == 0) __hip_atomic_store(&a.flags[(size_t)k * nR + g], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      stamp(ts + 3);
+      if (a.probe == 0 && tid < 9 && tid != 4) {
+        const int nry = ry + tid / 3 - 1, nrx = rx + tid % 3 - 1;
+        if (nry >= 0 && nry < a.rh && nrx >= 0 && nrx < a.rw) {
+          const unsigned* f = &a.flags[(size_t)k * nR + (size_t)nimg * R + nry * a.rw + nrx];
+          unsigned it = 0;
+          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            if (++it > kSpinLimit) {
+              failed = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+      }
+      __syncthreads();
+      stamp(ts + 4);
+      const __amdgpu_buffer_rsrc_t rlay = xrsrc(a.xbuf + (size_t)k * nR * (4 * 8 * C), (unsigned)nR * (4 * 8 * C * 4));
+      f32x4 hv[HK];
+#pragma unroll
+      for (int q = 0; q < HK; ++q)
+        hv[q] = hsrc[q] >= 0 && a.probe == 0 ? ld_sc1_16(rlay, hsrc[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < HK; ++q)
+        if (hlds[q] >= 0) *reinterpret_cast<f32x4*>(&tile[hlds[q]]) = hv[q];
+      __syncthreads();
+      stamp(ts + 5);
+    } else {
+      // a single region per patch: the halo is all outside the image
+      for (int e = tid; e < 36 * 16; e += NTH) {
+        const int hp = e >> 4, q = e & 15;
+        int hy, hx;
+        if (hp < 10) hy = -1, hx = hp - 1;
+        else if (hp < 20) hy = 8, hx = hp - 11;
+        else if (hp < 28) hy = hp - 20, hx = -1;
+        else hy = hp - 28, hx = 8;
+        *reinterpret_cast<f32x4*>(&tile[tpix(hy + 1, hx + 1) + 4 * q]) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+    }
+  };
+
+  // ---- the stride-2 layers' implicit GEMM (HEAD / TAIL): conv3x3_kernel's weight packing and
+  // step order; wave w owns 16 output pixels (rows 2 (w % 4), +1 of the region: lane li ->
+  // row (li >> 3), column li % 8) x output-channel blocks 2 (w / 4), +1 ----
+  const int dnb = wv & 3, dmb = (wv >> 2) * 2;
+  const int dry = 2 * dnb + (li >> 3), drx = li & 7;  // this lane's pixel in the region
+  auto dsrc = [&](const float* w) { return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(w), (short)0, 9 * C * C * 4, 0x00020000); };
+  auto dglob = [&](const __amdgpu_buffer_rsrc_t& r, int s, int m) -> f32x4 {
+    const int tap = s / KC, kc = s % KC;  // step s: tap-major, then the 16-channel chunk
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, (lg * C + (dmb + m) * 16 + li) * 16,
+                                                          ((tap * KC + kc) * 4 * C * 4) * 4, 0);
+    return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+  };
+
+  if constexpr (HEAD) {
+    // ---- the head: stage the input window of rows 2 oy0 - hpad + r, columns 2 ox0 - hpad + c
+    // (r, c < 17; zero outside = SAME padding), columns split by parity ----
+    float* const hw = smem + TILE;
+    const __amdgpu_buffer_rsrc_t hws = dsrc(a.head.wu);
+    constexpr int DPF = 2, DSTEP = 9 * KC;
+    f32x4 dav[DPF + 1][2];
+#pragma unroll
+    for (int p = 0; p < DPF; ++p)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) dav[p][m] = dglob(hws, p, m);
+    {
+      constexpr int NCH = HWR * 17 * (C / 4);  // 16-byte chunks
+      constexpr int NIT = (NCH + NTH - 1) / NTH;
+      const int iy0 = 2 * oy0 - a.hpad, ix0 = 2 * ox0 - a.hpad;
+      f32x4 tmp[NIT];
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const int e = i * NTH + tid;
+        tmp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e < NCH) {
+          const int c4 = e % 16, pe = e / 16, col = pe % 17, row = pe / 17;
+          const int iy = iy0 + row, ix = ix0 + col;
+          if (iy >= 0 && iy < a.hH && ix >= 0 && ix < a.hW)
+            tmp[i] = *reinterpret_cast<const f32x4*>(a.head_in + ((size_t)(nimg * a.hH + iy) * a.hW + ix) * C + c4 * 4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const int e = i * NTH + tid;
+        if (e < NCH) {
+          const int c4 = e % 16, pe = e / 16, col = pe % 17, row = pe / 17;
+          *reinterpret_cast<f32x4*>(&hw[(row * HWC + (col & 1) * 9 + (col >> 1)) * PS + c4 * 4]) = tmp[i];
+        }
+      }
+    }
+    __syncthreads();
+    stamp(CH_HEAD_TS);
+    f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    auto hload = [&](int s) -> f32x4 {
+      const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
+      const int pix = (2 * dry + ky) * HWC + (kx & 1) * 9 + drx + (kx >> 1);
+      return *reinterpret_cast<const f32x4*>(&hw[pix * PS + kc * 16 + lg * 4]);
+    };
+    f32x4 bq[2];
+    bq[0] = hload(0);
+#pragma unroll
+    for (int s = 0; s < DSTEP; ++s) {
+      if (s + DPF < DSTEP) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) dav[(s + DPF) % (DPF + 1)][m] = dglob(hws, s + DPF, m);
+      }
+      if (s + 1 < DSTEP) bq[(s + 1) & 1] = hload(s + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) dacc[m] = mfma4(dav[s % (DPF + 1)][m][t], bq[s & 1][t], dacc[m]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the first chain layer's weights fly during the head's epilogue and hand-off
+    {
+      const __amdgpu_buffer_rsrc_t w0 = wsrc(0);
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(w0, p, nb);
+    }
+    stamp(CH_HEAD_TS + 1);
+    // + bias, ReLU (conv3x3_kernel's epilogue), into the block-input tile and the border record
+    const __amdgpu_buffer_rsrc_t rpub = pub_rsrc(0);
+    const bool in_img = oy0 + dry < H && ox0 + drx < W;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int co = (dmb + m) * 16 + lg * 4;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(a.head.bias + co);
+      f32x4 v = dacc[m];
+      v.x = __fadd_rn(v.x, bb.x);
+      v.y = __fadd_rn(v.y, bb.y);
+      v.z = __fadd_rn(v.z, bb.z);
+      v.w = __fadd_rn(v.w, bb.w);
+      if (a.head.act == ACT_RELU) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      }
+      if (!in_img) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(&src[tpix(dry + 1, drx + 1) + co]) = v;
+      if (handoff_on) publish(rpub, dry, drx, co, v);
+    }
+    if (handoff_on) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // (also: every wave is done reading the window the next tiles alias)
+    stamp(CH_HEAD_TS + 2);
+    handoff(0, src, CH_HEAD_TS);
+  } else {
+    {
+      const __amdgpu_buffer_rsrc_t w0 = wsrc(0);
+#pragma unroll
+      for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(w0, p, nb);
+    }
+    // ---- stage the first layer's input tile (zero outside the image = SAME padding) ----
     constexpr int NSTAGE = LR * 10 * (C / 4);  // 1600 16-byte chunks
     constexpr int NIT = (NSTAGE + NTH - 1) / NTH;
     f32x4 tmp[NIT];
@@ -217,8 +453,8 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         *reinterpret_cast<f32x4*>(&src[tpix(row, col) + c4 * 4]) = tmp[i];
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
   stamp(1);
 
   // B^T row xi from input rows iA, iB of each tile (conv3x3_wino_kernel's exact signs)
@@ -235,39 +471,6 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   const int ay0 = WH == 1 ? 0 : tid >> 8;
   constexpr int nay = WH == 1 ? 2 : 1;
   const int ety = et / TTX, etx = et % TTX;
-  bool failed = false;
-
-  // halo descriptors of this thread, the same for every layer: the LDS offset in the tile and
-  // the byte offset of the neighbour's border record entry inside a layer's hand-off buffer
-  // (-1: outside the image, zero)
-  constexpr int HK = (36 * 16 + NTH - 1) / NTH;
-  int hlds[HK], hsrc[HK];
-#pragma unroll
-  for (int k = 0; k < HK; ++k) {
-    const int e = k * NTH + tid;
-    hlds[k] = hsrc[k] = -1;
-    if (e < 36 * 16) {
-      const int hp = e >> 4, q = e & 15;
-      int hy, hx;
-      if (hp < 10) hy = -1, hx = hp - 1;
-      else if (hp < 20) hy = 8, hx = hp - 11;
-      else if (hp < 28) hy = hp - 20, hx = -1;
-      else hy = hp - 28, hx = 8;
-      hlds[k] = tpix(hy + 1, hx + 1) + 4 * q;
-      const int gy = oy0 + hy, gx = ox0 + hx;
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const int nry = ry + (hy < 0 ? -1 : (hy > 7 ? 1 : 0)), nrx = rx + (hx < 0 ? -1 : (hx > 7 ? 1 : 0));
-        const int ny = hy & 7, nx = hx & 7;  // pixel inside the neighbour region
-        int side, idx;
-        if (hy < 0) side = 1, idx = nx;
-        else if (hy > 7) side = 0, idx = nx;
-        else if (hx < 0) side = 3, idx = ny;
-        else side = 2, idx = ny;
-        const int gn = nimg * R + nry * a.rw + nrx;
-        hsrc[k] = (gn * (4 * 8 * C) + (side * 8 + idx) * C + 4 * q) * 4;
-      }
-    }
-  }
 
   for (int l = 0; l < a.nl; ++l) {
     const bool last = l == a.nl - 1;
@@ -399,7 +602,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       }
     }
 
-    if (last) {  // ---- the chain's output: global f32 or the quantiser ----
+    if (last && !TAIL) {  // ---- the chain's output: global f32 or the quantiser ----
 #pragma unroll
       for (int k = 0; k < nay; ++k)
 #pragma unroll
@@ -421,12 +624,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       break;
     }
 
-    // ---- into the next layer's tile (interior), zero outside the image; a border pixel is
-    // published from the same registers (16-byte write-through stores into this region's 8 KB
-    // record: side 0 / 1 = rows 0 / 7, side 2 / 3 = columns 0 / 7; corners go to two sides) ----
-    const bool handoff = R > 1 && a.probe != 1;
-    const size_t g = (size_t)nimg * R + reg;
-    const __amdgpu_buffer_rsrc_t rpub = xrsrc(a.xbuf + ((size_t)l * nR + g) * (4 * 8 * C), 4 * 8 * C * 4);
+    // ---- into the next layer's (TAIL: the tail's) tile, zero outside the image; a border
+    // pixel is published from the same registers ----
+    const __amdgpu_buffer_rsrc_t rpub = pub_rsrc(KH + l);
     if (xch == dst) __syncthreads();  // every thread has read its T from dst's space
 #pragma unroll
     for (int k = 0; k < nay; ++k)
@@ -436,64 +636,81 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         const bool in_img = oy0 + ly < H && ox0 + lx < W;
         const f32x4 v = in_img ? y[k][b] : f32x4{0.f, 0.f, 0.f, 0.f};
         *reinterpret_cast<f32x4*>(&dst[tpix(ly + 1, lx + 1) + co]) = v;
-        if (handoff) {
-          if (ly == 0) st_sc1_16(rpub, ((0 * 8 + lx) * C + co) * 4, v);
-          if (ly == 7) st_sc1_16(rpub, ((1 * 8 + lx) * C + co) * 4, v);
-          if (lx == 0) st_sc1_16(rpub, ((2 * 8 + ly) * C + co) * 4, v);
-          if (lx == 7) st_sc1_16(rpub, ((3 * 8 + ly) * C + co) * 4, v);
-        }
+        if (handoff_on) publish(rpub, ly, lx, co, v);
       }
-    if (handoff) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (handoff_on) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     stamp(ts + 2);
+    handoff(KH + l, dst, ts);
+    src = dst;
+  }
 
-    // ---- hand-off: raise this region's flag, then read the neighbours' borders ----
-    if (handoff) {
-      if (tid == 0) __hip_atomic_store(&a.flags[(size_t)l * nR + g], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      stamp(ts + 3);
-      // wait for the (up to 8) neighbours' flags of this layer
-      if (a.probe == 0 && tid < 9 && tid != 4) {
-        const int nry = ry + tid / 3 - 1, nrx = rx + tid % 3 - 1;
-        if (nry >= 0 && nry < a.rh && nrx >= 0 && nrx < a.rw) {
-          const unsigned* f = &a.flags[(size_t)l * nR + (size_t)nimg * R + nry * a.rw + nrx];
-          unsigned it = 0;
-          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            if (++it > kSpinLimit) {
-              failed = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
+  if constexpr (TAIL) {
+    // ---- the tail: conv3x3_kernel<MODE_T2> on the run's last output (src, halo filled):
+    // input position (dry, drx) of the region feeds output phase ph = 2 (ky == 1) + (kx == 1)
+    // through input offset (-(ky == 2), -(kx == 2)) ----
+    stamp(CH_TAIL_TS);
+    const __amdgpu_buffer_rsrc_t tws = dsrc(a.tail.wu);
+    constexpr int DPF = 2, DSTEP = 9 * KC;
+    f32x4 dav[DPF + 1][2];
+#pragma unroll
+    for (int p = 0; p < DPF; ++p)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) dav[p][m] = dglob(tws, p, m);
+    f32x4 tacc[4][2];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) tacc[p][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto tload = [&](int s) -> f32x4 {
+      const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
+      return *reinterpret_cast<const f32x4*>(&src[tpix(dry + 1 - (ky == 2), drx + 1 - (kx == 2)) + kc * 16 + lg * 4]);
+    };
+    f32x4 bq[2];
+    bq[0] = tload(0);
+#pragma unroll
+    for (int s = 0; s < DSTEP; ++s) {
+      const int tap = s / KC, ky = tap / 3, kx = tap % 3;
+      const int ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
+      if (s + DPF < DSTEP) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) dav[(s + DPF) % (DPF + 1)][m] = dglob(tws, s + DPF, m);
+      }
+      if (s + 1 < DSTEP) bq[(s + 1) & 1] = tload(s + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) tacc[ph][m] = mfma4(dav[s % (DPF + 1)][m][t], bq[s & 1][t], tacc[ph][m]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    stamp(CH_TAIL_TS + 1);
+    // + bias, act (conv3x3_kernel's epilogue), 16-byte f32 stores of the 16x16 output tile
+    if (oy0 + dry < H && ox0 + drx < W) {
+      const int Ho = 2 * H, Wo = 2 * W;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int oy = 2 * (oy0 + dry) + (p >> 1), ox = 2 * (ox0 + drx) + (p & 1);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const int co = (dmb + m) * 16 + lg * 4;
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(a.tail.bias + co);
+          f32x4 v = tacc[p][m];
+          v.x = __fadd_rn(v.x, bb.x);
+          v.y = __fadd_rn(v.y, bb.y);
+          v.z = __fadd_rn(v.z, bb.z);
+          v.w = __fadd_rn(v.w, bb.w);
+          if (a.tail.act == ACT_RELU) {
+            v.x = fmaxf(v.x, 0.f);
+            v.y = fmaxf(v.y, 0.f);
+            v.z = fmaxf(v.z, 0.f);
+            v.w = fmaxf(v.w, 0.f);
           }
+          *reinterpret_cast<f32x4*>(a.tail_out + ((size_t)(nimg * Ho + oy) * Wo + ox) * C + co) = v;
         }
       }
-      __syncthreads();
-      stamp(ts + 4);
-      // halo ring of dst: rows 0 and 9 (10 px each), columns 0 and 9 (rows 1..8): 36 px x 16
-      // quads, from the descriptors computed once before the layer loop (all loads first)
-      const __amdgpu_buffer_rsrc_t rlay = xrsrc(a.xbuf + (size_t)l * nR * (4 * 8 * C), (unsigned)nR * (4 * 8 * C * 4));
-      f32x4 hv[HK];
-#pragma unroll
-      for (int k = 0; k < HK; ++k)
-        hv[k] = hsrc[k] >= 0 && a.probe == 0 ? ld_sc1_16(rlay, hsrc[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < HK; ++k)
-        if (hlds[k] >= 0) *reinterpret_cast<f32x4*>(&dst[hlds[k]]) = hv[k];
-      __syncthreads();
-      stamp(ts + 5);
-    } else {
-      // a single region per patch: the halo is all outside the image
-      for (int e = tid; e < 36 * 16; e += NTH) {
-        const int hp = e >> 4, q = e & 15;
-        int hy, hx;
-        if (hp < 10) hy = -1, hx = hp - 1;
-        else if (hp < 20) hy = 8, hx = hp - 11;
-        else if (hp < 28) hy = hp - 20, hx = -1;
-        else hy = hp - 28, hx = 8;
-        *reinterpret_cast<f32x4*>(&dst[tpix(hy + 1, hx + 1) + 4 * q]) = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      __syncthreads();
     }
-    src = dst;
+    stamp(CH_TAIL_TS + 2);
   }
 
   // ---- the last workgroup to finish resets the ticket and advances the epoch ----

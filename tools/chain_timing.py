@@ -52,6 +52,22 @@ def summarise(t, nl):
             d = us(t[:, marks[k + 1]] - t[:, marks[k]])
             row[PHASES[k]] = [round(float(np.median(d)), 2), round(float(np.percentile(d, 90)), 2)]
         rep["layers"].append(row)
+    # the stride-2 head / transposed tail of a chain_x launch (wino_chain.h CH_HEAD_TS / CH_TAIL_TS:
+    # stamps after the 8 layer slots)
+    hb = 2 + 6 * 8
+    if t.shape[1] >= hb + 12:
+        if np.all(t[:, hb + 5] != 0):
+            marks = [0] + [hb + k for k in range(6)]
+            names = ["window", "mfma", "epilogue", "publish", "wait", "halo"]
+            rep["head"] = {names[k]: [round(float(np.median(us(t[:, marks[k + 1]] - t[:, marks[k]]))), 2),
+                                      round(float(np.percentile(us(t[:, marks[k + 1]] - t[:, marks[k]]), 90)), 2)]
+                           for k in range(6)}
+        tb = hb + 6
+        if np.all(t[:, tb + 2] != 0):
+            rep["tail"] = {nm: [round(float(np.median(us(t[:, tb + k + 1] - t[:, tb + k]))), 2),
+                                round(float(np.percentile(us(t[:, tb + k + 1] - t[:, tb + k]), 90)), 2)]
+                           for k, nm in enumerate(["mfma", "store"])}
+            rep["kernel_us"] = round(float(us(t[:, tb + 2].max() - start.min())), 2)
     return rep
 
 
@@ -81,6 +97,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64, help="patches per call (one lane: the per-launch batch)")
     ap.add_argument("--enc01", action="store_true")
     ap.add_argument("--chain-wh", type=int, default=0, help="chain workgroup shape (option chain_wh), 0: the tuning's")
+    ap.add_argument("--chain-x", type=int, default=-1, help="option chain_x (stride-2 head / tail), -1: the tuning's")
     args = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "chain_ts.bin")
     os.environ["TIC_ENC01_TIMING" if args.enc01 else "TIC_CHAIN_TIMING"] = path
@@ -97,6 +114,8 @@ def main():
         c.set_option("chain", 1)
         if args.chain_wh:
             c.set_option("chain_wh", args.chain_wh)
+        if args.chain_x >= 0:
+            c.set_option("chain_x", args.chain_x)
     eh, ew, ec = bottleneck_shape(M, P)
     x = np.random.default_rng(1234).integers(0, 256, (B, P, P, 3), dtype=np.uint8)
     d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(B * eh * ew * ec), c.alloc(x.nbytes)
