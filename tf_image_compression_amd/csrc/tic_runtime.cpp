@@ -654,13 +654,15 @@ const int kRgbInDefault = 2;   // TH 16
 // they apply (bit-identical, measured faster for model_0 and model_3 by tic_autotune_step:
 // profiles/tune logs in DESIGN.md §3), the stride-1 chain where the runs are small 16x16
 // stages (model_0/1/2: measured faster) but not for model_3's 64x64 / 32x32 stages or the
-// rmbe net (the step tuner keeps it off there).
+// rmbe net (the step tuner keeps it off there), and with it the stride-2 head / transposed tail
+// ("chain_x", env TIC_CHAIN_X: model_0 step -3.1 % in alternating A/B, profiles/
+// ab_r05_chain_x_m0.json).
 struct StructDefaults {
   bool fuse01, fuse_tail, chain, chain_x;
 };
 StructDefaults struct_defaults(int model_id) {
   const bool small_stages = model_id == 0 || model_id == 1 || model_id == 2;
-  return {true, true, small_stages, false};
+  return {true, true, small_stages, small_stages};
 }
 
 // Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino|wino4, else built-in:

@@ -328,6 +328,10 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     for (int p = 0; p < DPF; ++p)
 #pragma unroll
       for (int m = 0; m < 2; ++m) dav[p][m] = dglob(hws, p, m);
+    // the epilogue's biases, loaded now (after the K loop their latency would be exposed)
+    f32x4 hbias[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) hbias[m] = *reinterpret_cast<const f32x4*>(a.head.bias + (dmb + m) * 16 + lg * 4);
     {
       constexpr int NCH = HWR * 17 * (C / 4);  // 16-byte chunks
       constexpr int NIT = (NCH + NTH - 1) / NTH;
@@ -392,7 +396,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
       const int co = (dmb + m) * 16 + lg * 4;
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(a.head.bias + co);
+      const f32x4 bb = hbias[m];
       f32x4 v = dacc[m];
       v.x = __fadd_rn(v.x, bb.x);
       v.y = __fadd_rn(v.y, bb.y);
@@ -657,6 +661,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     for (int p = 0; p < DPF; ++p)
 #pragma unroll
       for (int m = 0; m < 2; ++m) dav[p][m] = dglob(tws, p, m);
+    f32x4 tbias[2];  // loaded before the K loop (latency hidden behind it)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) tbias[m] = *reinterpret_cast<const f32x4*>(a.tail.bias + (dmb + m) * 16 + lg * 4);
     f32x4 tacc[4][2];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -694,7 +701,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
           const int co = (dmb + m) * 16 + lg * 4;
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(a.tail.bias + co);
+          const f32x4 bb = tbias[m];
           f32x4 v = tacc[p][m];
           v.x = __fadd_rn(v.x, bb.x);
           v.y = __fadd_rn(v.y, bb.y);
