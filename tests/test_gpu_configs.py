@@ -255,11 +255,13 @@ def test_graph_replay_after_workspace_growth():
         c.set_option("graph", 0)
 
 
-@pytest.mark.parametrize("mark", ["encode_0", "encode_res_1/conv_0", "decode_1", "encode_3"])
-def test_mark_layer_in_step_timing(mark):
+@pytest.mark.parametrize("mark,chain_x", [("encode_0", 1), ("encode_res_1/conv_0", 0), ("decode_1", 1),
+                                          ("encode_3", 0), ("encode_3", 1)])
+def test_mark_layer_in_step_timing(mark, chain_x):
     """bench.py's in-step launch timing (option mark_layer + tic_mark_durations): one event
     pair per lane per call around the launch that starts at the marked layer — a fused
-    pair, a chain run or a plain layer — and the results stay bit-identical."""
+    pair, a chain run, a chain run with its stride-2 head (chain_x: the launch starts at
+    encode_3) or a plain layer — and the results stay bit-identical."""
     from tf_image_compression_amd.codec import Codec
     from tf_image_compression_amd.topology import layer_table
     from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
@@ -269,6 +271,7 @@ def test_mark_layer_in_step_timing(mark):
         c.set_option("fuse01", 1)
         c.set_option("fuse_tail", 1)
         c.set_option("chain", 1)
+        c.set_option("chain_x", chain_x)
         x = structured_patches(n, P, seed=520)
         eh, ew, ec = c.code_shape
         d_in, d_idx, d_rgb = c.alloc(x.nbytes), c.alloc(n * eh * ew * ec), c.alloc(x.nbytes)

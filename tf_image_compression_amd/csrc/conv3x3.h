@@ -959,11 +959,20 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
     }
     if constexpr (CMP) {
       __syncthreads();  // every wave is done with the RGB planes the tile overwrites
+      if (inner0) {  // workgroup-uniform: no slot of the tile lies in layer 1's zero padding
 #pragma unroll
-      for (int jb = 0; jb < NPW; ++jb) {
-        const int blk = wave + 4 * jb;
-        if (blk < 2 * LR1) put0_main(jb, inner0 || blk_valid(blk), res[jb]);
-        else if (blk < NBL && blk_has(blk)) put0(blk_slot(blk), blk_valid(blk), res[jb]);
+        for (int jb = 0; jb < NPW; ++jb) {
+          const int blk = wave + 4 * jb;
+          if (blk < 2 * LR1) put0_main(jb, true, res[jb]);
+          else if (blk < NBL && blk_has(blk)) put0(blk_slot(blk), true, res[jb]);
+        }
+      } else {
+#pragma unroll
+        for (int jb = 0; jb < NPW; ++jb) {
+          const int blk = wave + 4 * jb;
+          if (blk < 2 * LR1) put0_main(jb, blk_valid(blk), res[jb]);
+          else if (blk < NBL && blk_has(blk)) put0(blk_slot(blk), blk_valid(blk), res[jb]);
+        }
       }
     }
   }
