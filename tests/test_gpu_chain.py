@@ -221,3 +221,32 @@ def test_wino_chain_stride2_neighbours_oversubscribed():
             assert all(np.array_equal(idx[i * 8:(i + 1) * 8], ref_idx) for i in range(64))
         u8 = c.decode(idx)
         assert all(np.array_equal(u8[i * 8:(i + 1) * 8], ref_u8) for i in range(64))
+
+
+@pytest.mark.parametrize("model_id,P,n", [(0, 256, 6), (0, 64, 5), (0, 48, 3), (1, 64, 4), (0, 288, 2)])
+def test_wino_chain_decode2_behind_tail_bit_identical(model_id, P, n):
+    """chain_x 2: decode_2 (transposed 64 -> 32) runs in the decoder chain's launch as well,
+    on decode_3's output kept in LDS; decode_3's outputs just above / left of a region are
+    recomputed from the run's halo ring in conv3x3_kernel's order (as dec10 does for decode_1),
+    so everything stays bit-identical to the unfused launches: 2x2 regions (P = 256), one
+    region (P = 64), one partial region (P = 48), 3x3 regions with partial ones at the bottom
+    and right (P = 288).  Reference layers: model_0/model.py:198-222 (decode_3, decode_2)."""
+    with _codec(model_id, P) as c:
+        x = structured_patches(n, P, seed=770 + model_id + P)
+        c.set_option("s1_form", 1)
+        c.set_option("chain", 0)
+        ref = _run(c, x)
+        c.set_option("chain", 1)
+        c.set_option("chain_wh", 2)
+        c.set_option("chain_x", 2)
+        names = [lay[0] for lay in c.layers()]
+        for streams in (1, 2):
+            c.set_option("streams", streams)
+            kern = c.layer_kernels(n)
+            assert any(re.fullmatch(r"wino_chain_kernel<\d,\d,2,6>", k) for k in kern), kern
+            assert kern[names.index("decode_3")] == "" and kern[names.index("decode_2")] == "", kern
+            got = _run(c, x)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b)
+        c.set_option("chain_x", 1)
+        assert not any(re.fullmatch(r"wino_chain_kernel<\d,\d,2,6>", k) for k in c.layer_kernels(n))

@@ -454,9 +454,10 @@ struct tic_handle {
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
-  bool chain_x = false;    // the stride-2 neighbours of a run inside its launch (option "chain_x":
-                           // the encoder's stride-2 layer in front as the head, the decoder's
-                           // transposed layer behind as the tail; wino_chain.h HT)
+  int chain_x = 0;         // the stride-2 neighbours of a run inside its launch (option "chain_x":
+                           // 1 the encoder's stride-2 layer in front as the head, the decoder's
+                           // transposed layer behind as the tail; 2 also the decoder's next
+                           // transposed layer (decode_2) behind the tail; wino_chain.h HT)
   int chain_order = -1;    // chain region order (option "chain_order"): 0 atomic ticket, 1 blockIdx,
                            // 2 blockIdx XCD-aware, -1 auto: 2 when every lane's chain grid is
                            // resident at once, else 0 (chain_launch_order)
@@ -658,11 +659,12 @@ const int kRgbInDefault = 2;   // TH 16
 // ("chain_x", env TIC_CHAIN_X: model_0 step -3.1 % in alternating A/B, profiles/
 // ab_r05_chain_x_m0.json).
 struct StructDefaults {
-  bool fuse01, fuse_tail, chain, chain_x;
+  bool fuse01, fuse_tail, chain;
+  int chain_x;
 };
 StructDefaults struct_defaults(int model_id) {
   const bool small_stages = model_id == 0 || model_id == 1 || model_id == 2;
-  return {true, true, small_stages, small_stages};
+  return {true, true, small_stages, small_stages ? 1 : 0};
 }
 
 // Stride-1 form policy (like the last layer's): TIC_S1_FORM=direct|wino|wino4, else built-in:
@@ -793,8 +795,8 @@ static int chain_launch_order(const tic_handle* h, int n, int R) {
 // argument for more than the run's own layers.
 struct ChainSpan {
   int start = -1, s1 = -1, end = -1;
-  bool head = false, tail = false;
-  int last() const { return end - 1 + (tail ? 1 : 0); }
+  bool head = false, tail = false, tail2 = false;
+  int last() const { return end - 1 + (tail ? 1 : 0) + (tail2 ? 1 : 0); }
   bool valid() const { return start >= 0; }
 };
 static bool s2_64_relu(const LayerDef& d, int kind) {
@@ -824,6 +826,12 @@ static ChainSpan chain_span_at(const tic_handle* h, int li) {
   sp.tail = ce < L - 1 && s2_64_relu(h->layers[ce].def, K_T2) && !(ce >= L - 2 && fuses_tail(h)) &&
             (h->rmbe() || ce > h->n_enc) && h->layers[ce].h_in == h->layers[s1].h_in &&
             chain_x_fits(h, h->layers[s1].h_in);
+  // chain_x 2: decode_2 (transposed 64 -> 32, ReLU) behind the tail, not the fused tail's
+  if (sp.tail && h->chain_x >= 2 && ce + 1 < L - 1 && !(ce + 1 >= L - 2 && fuses_tail(h))) {
+    const LayerDef& d2 = h->layers[ce + 1].def;
+    sp.tail2 = d2.kind == K_T2 && d2.cin == 64 && d2.cout == 32 && d2.act == 1 && !d2.residual &&
+               h->layers[ce + 1].h_in == 2 * h->layers[s1].h_in;
+  }
   return sp;
 }
 // every chain launch of the network, in order (as run_layers walks it)
@@ -845,10 +853,10 @@ static bool in_chain(const tic_handle* h, int i) {
   return false;
 }
 static bool any_chain(const tic_handle* h) { return !chain_spans(h).empty(); }
-// whether the option "chain_x" changes the launch plan at all
-static bool any_chain_x(const tic_handle* h) {
+// whether the option "chain_x" changes the launch plan at all (level 2: a decode_2 behind a tail)
+static bool any_chain_x(const tic_handle* h, int level = 1) {
   for (const ChainSpan& sp : chain_spans(h))
-    if (sp.head || sp.tail) return true;
+    if (level >= 2 ? sp.tail2 : (sp.head || sp.tail)) return true;
   return false;
 }
 
@@ -1026,13 +1034,18 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         a.tail = {tl.d_w, tl.d_b, tl.def.act, 0};
         a.tail_out = ws[dst];
       }
+      if (sp.tail2) {  // and the next one (decode_2), whose output is the next activation instead
+        const LayerRT& tl2 = h->layers[ce + 1];
+        a.tail2 = {tl2.d_w, tl2.d_b, tl2.def.act, 0};
+        a.tail2_out = ws[dst];
+      }
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
       if (getenv("TIC_CHAIN_TIMING")) {  // phase timestamps of this launch (tools/chain_timing.py)
         int rc2 = probe_stamps(ln, first_dec_c || sp.tail ? 1 : 0, n * R, st, &a.tstamp);
         if (rc2) return rc2;
       }
       const int inm = first_dec_c ? tic::IN_IDX : tic::IN_F32, outm = last_enc_c ? tic::OUT_QUANT : tic::OUT_F32;
-      const int ht = (sp.head ? tic::CH_HEAD : 0) | (sp.tail ? tic::CH_TAIL : 0);
+      const int ht = (sp.head ? tic::CH_HEAD : 0) | (sp.tail ? tic::CH_TAIL : 0) | (sp.tail2 ? tic::CH_TAIL2 : 0);
       if (!tic::launch_wino_chain(inm, outm, a, st, h->chain_wh, ht))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, sp.last());
       rc = check_launch();
@@ -1415,7 +1428,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* f = getenv("TIC_FUSE_TAIL")) h->fuse_tail = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN")) h->chain = atoi(f) != 0;
   if (const char* f = getenv("TIC_CHAIN_WH")) h->chain_wh = std::min(2, std::max(1, atoi(f)));
-  if (const char* f = getenv("TIC_CHAIN_X")) h->chain_x = atoi(f) != 0;
+  if (const char* f = getenv("TIC_CHAIN_X")) h->chain_x = std::min(2, std::max(0, atoi(f)));
   if (const char* f = getenv("TIC_CHAIN_ORDER")) h->chain_order = std::min(2, std::max(-1, atoi(f)));
   if (const char* f = getenv("TIC_DECOUPLE")) h->decouple = atoi(f) != 0;
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -1799,11 +1812,11 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     h->chain_wh = value;
     return TIC_OK;
   }
-  if (k == "chain_x") {  // the stride-2 neighbours of a run in its launch (head / tail)
-    if (value < -1 || value > 1) return fail(TIC_EINVAL, "chain_x must be -1, 0 or 1");
+  if (k == "chain_x") {  // the stride-2 neighbours of a run in its launch (1 head / tail, 2 + decode_2)
+    if (value < -1 || value > 2) return fail(TIC_EINVAL, "chain_x must be -1, 0, 1 or 2");
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
-    h->chain_x = value < 0 ? struct_defaults(h->model_id).chain_x : value != 0;
+    h->chain_x = value < 0 ? struct_defaults(h->model_id).chain_x : value;
     return TIC_OK;
   }
   if (k == "chain_order") {  // 0 atomic ticket, 1 blockIdx, 2 blockIdx XCD-aware, -1 auto
@@ -2193,13 +2206,19 @@ int tic_autotune_step(tic_handle* h, const void* d_in, int n, int rounds, int re
     clear_graphs(h);
   }
   if (!rc && h->chain && !getenv("TIC_CHAIN_X")) {  // the stride-2 neighbours inside the chain's launch
-    const bool was = h->chain_x;
-    h->chain_x = true;
-    const bool can = any_chain_x(h);
-    h->chain_x = was;
-    bool keep = false;
-    if (can) rc = confirm([&](bool alt) { h->chain_x = alt ? !was : was; }, 0.005f, "chain_x", &keep, &cur);
-    clear_graphs(h);
+    // first head / tail against none, then decode_2 behind the tail against head / tail only
+    for (int level = 1; level <= 2 && !rc; ++level) {
+      const int was = h->chain_x;
+      const int base = level - 1, alt_v = level;
+      h->chain_x = alt_v;
+      const bool can = any_chain_x(h, level);
+      h->chain_x = was;
+      if (!can || (was != base && was != alt_v)) continue;
+      const int other = was == base ? alt_v : base;
+      bool keep = false;
+      rc = confirm([&](bool alt) { h->chain_x = alt ? other : was; }, 0.005f, "chain_x", &keep, &cur);
+      clear_graphs(h);
+    }
   }
   const int L = (int)h->layers.size();
   for (int round = 0; round < rounds && !rc; ++round) {
@@ -2356,7 +2375,7 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   if (cs.valid()) {
     if (cs.start == i) {
       const bool first_dec = !h->rmbe() && cs.s1 == h->n_enc, last_enc = !h->rmbe() && cs.end - 1 == h->n_enc - 1;
-      const int ht = (cs.head ? tic::CH_HEAD : 0) | (cs.tail ? tic::CH_TAIL : 0);
+      const int ht = (cs.head ? tic::CH_HEAD : 0) | (cs.tail ? tic::CH_TAIL : 0) | (cs.tail2 ? tic::CH_TAIL2 : 0);
       snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh,
                ht);
     }
@@ -2471,7 +2490,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       else if (!strcmp(name, "s1_form") && a >= 0 && a <= 2) s1_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
       else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 2) chain_wh = a;
-      else if (!strcmp(name, "chain_x")) chain_x = a != 0;
+      else if (!strcmp(name, "chain_x") && a >= 0 && a <= 2) chain_x = a;
       else return fail(TIC_EINVAL, "tuning line %d: unknown flag %s", line, name);
     } else if (!strcmp(kind, "conv")) {
       if (sscanf(ln.c_str(), "conv %d %d %d %d", &a, &b, &c, &d) != 4 || a < 0 || a >= L || c < 0 || c > 2)

@@ -52,7 +52,7 @@ constexpr int CH_MAX_LAYERS = 8;
 // tail's (start, K loop done, stores issued)
 constexpr int CH_TS = 2 + 6 * (CH_MAX_LAYERS + 2);
 constexpr int CH_HEAD_TS = 2 + 6 * CH_MAX_LAYERS, CH_TAIL_TS = CH_HEAD_TS + 6;
-constexpr int CH_HEAD = 1, CH_TAIL = 2;  // HT bits
+constexpr int CH_HEAD = 1, CH_TAIL = 2, CH_TAIL2 = 4;  // HT bits (CH_TAIL2 needs CH_TAIL)
 
 struct ChainLayer {
   const float* wu;    // Winograd U [16 p][4 kc][4 g][64][4 t] (pack_wino)
@@ -93,6 +93,11 @@ struct ChainArgs {
   // [n, 2H, 2W, 64] to tail_out.
   ChainLayer tail;
   float* tail_out;
+  // HT & CH_TAIL2: the next transposed layer too (decode_2, 64 -> 32; direct packing with
+  // Cout 32): the tail's output stays in LDS as its input (the halo row / column recomputed
+  // from the run's halo ring), it writes f32 [n, 4H, 4W, 32] to tail2_out.
+  ChainLayer tail2;
+  float* tail2_out;
 };
 
 namespace chain {
@@ -147,7 +152,8 @@ template <int IN, int OUT, int WH = 1, int HT = 0>
 __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(const ChainArgs a) {
   using namespace chain;
   constexpr int NTH = 256 * WH;
-  constexpr bool HEAD = (HT & CH_HEAD) != 0, TAIL = (HT & CH_TAIL) != 0;
+  constexpr bool HEAD = (HT & CH_HEAD) != 0, TAIL = (HT & CH_TAIL) != 0, TAIL2 = (HT & CH_TAIL2) != 0;
+  static_assert(!TAIL2 || TAIL, "decode_2 runs on the tail's output");
   static_assert(HT == 0 || WH == 2, "stride-2 head / tail: 512-thread workgroups only");
   // WH = 2 (one workgroup per CU): the T exchange gets a buffer of its own beside the two
   // tiles, so it never aliases a tile and needs no barrier of its own
@@ -692,6 +698,171 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       __builtin_amdgcn_sched_barrier(0);
     }
     stamp(CH_TAIL_TS + 1);
+    if constexpr (TAIL2) {
+      // ---- decode_3's outputs stay on chip: they are decode_2's input tile T3 (17 x 17
+      // positions, row / column 0 = the outputs just above / left of the region's 16 x 16).
+      // Those halo outputs are recomputed here from the run's halo ring, in conv3x3_kernel's
+      // order for them (as dec10 does for decode_1): wave w, output-channel block w % 4,
+      // pass w / 4 — 0: the row above (input row -1, columns -1..7: phase (1,0) from taps 3
+      // then 5, phase (1,1) from tap 4), 1: the column left (input column -1, rows 0..7: phase
+      // (0,1) from taps 1 then 7, phase (1,1) from tap 4) ----
+      const int hm = wv & 3, hrow = (wv >> 2) == 0;
+      f32x4 hacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      {
+        const __amdgpu_buffer_rsrc_t r3 = dsrc(a.tail.wu);
+        const int lq = li < 9 ? li : 8;  // row pass: input column lq - 1; column pass: input row li (li < 8)
+#pragma unroll
+        for (int ti = 0; ti < 3; ++ti) {
+          const int tap = hrow ? 3 + ti : 1 + 3 * ti;  // ascending
+          const int ky = tap / 3, kx = tap % 3;
+          const int q = ti == 1 ? 1 : 0;  // the middle tap is tap 4 in both passes
+          int pix;
+          if (hrow) pix = tpix(0, max(lq - (kx == 2), 0));                       // input (-1, lq - 1 - (kx == 2))
+          else pix = tpix(min(li, 7) + 1 - (ky == 2), 0);                        // input (li - (ky == 2), -1)
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(&src[pix + kc * 16 + lg * 4]);
+            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r3, (lg * C + hm * 16 + li) * 16,
+                                                                  ((tap * KC + kc) * 4 * C * 4) * 4, 0);
+            const f32x4 w = f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) hacc[q] = mfma4(w[t], b[t], hacc[q]);
+          }
+        }
+      }
+      const f32x4 hb = *reinterpret_cast<const f32x4*>(a.tail.bias + hm * 16 + lg * 4);
+      __syncthreads();  // every wave is done reading the run's tiles: T3 aliases them
+      float* const t3 = smem;
+      constexpr int T3C = 17, PS3 = PS;
+      auto epi = [&](f32x4 v, const f32x4& bb, bool valid) {
+        v.x = __fadd_rn(v.x, bb.x);
+        v.y = __fadd_rn(v.y, bb.y);
+        v.z = __fadd_rn(v.z, bb.z);
+        v.w = __fadd_rn(v.w, bb.w);
+        if (a.tail.act == ACT_RELU) {
+          v.x = fmaxf(v.x, 0.f);
+          v.y = fmaxf(v.y, 0.f);
+          v.z = fmaxf(v.z, 0.f);
+          v.w = fmaxf(v.w, 0.f);
+        }
+        return valid ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      };
+      {  // the interior 16 x 16 (zero beyond the image: decode_2's padding)
+        const bool valid = oy0 + dry < H && ox0 + drx < W;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int oy = 2 * dry + (p >> 1), ox = 2 * drx + (p & 1);
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+            *reinterpret_cast<f32x4*>(&t3[((1 + oy) * T3C + 1 + ox) * PS3 + (dmb + m) * 16 + lg * 4]) =
+                epi(tacc[p][m], tbias[m], valid);
+        }
+      }
+      {  // the halo row / column (zero above / left of the image)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          int r, c;
+          bool use, valid;
+          if (hrow) {  // input column li - 1: phase (1, q) -> output (-1, 2 (li - 1) + q)
+            const int ox = 2 * (li - 1) + q;
+            r = 0, c = 1 + ox;
+            use = li < 9 && ox >= -1;
+            valid = oy0 > 0 && ox0 + (ox >> 1) >= 0 && ox0 + (ox >> 1) < W;
+          } else {  // input row li: phase (q, 1) -> output (2 li + q, -1)
+            const int oy = 2 * li + q;
+            r = 1 + oy, c = 0;
+            use = li < 8;
+            valid = ox0 > 0 && oy0 + li < H;
+          }
+          if (use) *reinterpret_cast<f32x4*>(&t3[(r * T3C + c) * PS3 + hm * 16 + lg * 4]) = epi(hacc[q], hb, valid);
+        }
+      }
+      __syncthreads();
+      stamp(CH_TAIL_TS + 2);
+      // ---- decode_2: conv3x3_kernel<MODE_T2, 64, 32> on T3; wave w owns input rows 2w, 2w + 1
+      // (16 positions each) x both 16-channel output blocks x the four phases ----
+      constexpr int C2 = 32;
+      const __amdgpu_buffer_rsrc_t w2s =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.tail2.wu), (short)0, 9 * C * C2 * 4, 0x00020000);
+      auto d2glob = [&](int s, int m) -> f32x4 {
+        const int tap = s / KC, kc = s % KC;
+        const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(w2s, (lg * C2 + m * 16 + li) * 16,
+                                                              ((tap * KC + kc) * 4 * C2 * 4) * 4, 0);
+        return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+      };
+      f32x4 b2[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) b2[m] = *reinterpret_cast<const f32x4*>(a.tail2.bias + m * 16 + lg * 4);
+      f32x4 e2[DPF + 1][2];
+#pragma unroll
+      for (int p = 0; p < DPF; ++p)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) e2[p][m] = d2glob(p, m);
+      f32x4 acc2[4][2][2];  // [phase][row of the wave][channel block]
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int m = 0; m < 2; ++m) acc2[p][j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto load2 = [&](int s, f32x4 (&dst2)[2]) {
+        const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          dst2[j] = *reinterpret_cast<const f32x4*>(
+              &t3[((1 + 2 * wv + j - (ky == 2)) * T3C + 1 + li - (kx == 2)) * PS3 + kc * 16 + lg * 4]);
+      };
+      f32x4 bq2[2][2];
+      load2(0, bq2[0]);
+#pragma unroll
+      for (int s = 0; s < DSTEP; ++s) {
+        const int tap = s / KC, ky = tap / 3, kx = tap % 3;
+        const int ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
+        if (s + DPF < DSTEP) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m) e2[(s + DPF) % (DPF + 1)][m] = d2glob(s + DPF, m);
+        }
+        if (s + 1 < DSTEP) load2(s + 1, bq2[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+              acc2[ph][j][m] = mfma4(e2[s % (DPF + 1)][m][t], bq2[s & 1][j][t], acc2[ph][j][m]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      stamp(CH_TAIL_TS + 3);
+      // + bias, act; decode_2's output [n, 4H, 4W, 32], 16-byte stores
+      const int H3 = 2 * H, W3 = 2 * W, Ho2 = 4 * H, Wo2 = 4 * W;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int gy = 2 * oy0 + 2 * wv + j, gx = 2 * ox0 + li;  // decode_2 input position
+        if (gy >= H3 || gx >= W3) continue;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int oy = 2 * gy + (p >> 1), ox = 2 * gx + (p & 1);
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            f32x4 v = acc2[p][j][m];
+            const f32x4 bb = b2[m];
+            v.x = __fadd_rn(v.x, bb.x);
+            v.y = __fadd_rn(v.y, bb.y);
+            v.z = __fadd_rn(v.z, bb.z);
+            v.w = __fadd_rn(v.w, bb.w);
+            if (a.tail2.act == ACT_RELU) {
+              v.x = fmaxf(v.x, 0.f);
+              v.y = fmaxf(v.y, 0.f);
+              v.z = fmaxf(v.z, 0.f);
+              v.w = fmaxf(v.w, 0.f);
+            }
+            *reinterpret_cast<f32x4*>(a.tail2_out + ((size_t)(nimg * Ho2 + oy) * Wo2 + ox) * C2 + m * 16 + lg * 4) = v;
+          }
+        }
+      }
+      stamp(CH_TAIL_TS + 4);
+    } else {
     // + bias, act (conv3x3_kernel's epilogue), 16-byte f32 stores of the 16x16 output tile
     if (oy0 + dry < H && ox0 + drx < W) {
       const int Ho = 2 * H, Wo = 2 * W;
@@ -718,6 +889,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       }
     }
     stamp(CH_TAIL_TS + 2);
+    }
   }
 
   // ---- the last workgroup to finish resets the ticket and advances the epoch ----

@@ -64,10 +64,13 @@ def summarise(t, nl):
                            for k in range(6)}
         tb = hb + 6
         if np.all(t[:, tb + 2] != 0):
+            # chain_x 2: decode_3 -> LDS tile (+ halo recompute), then decode_2's K loop and stores
+            two = np.all(t[:, tb + 4] != 0)
+            names = ["mfma", "halo+tile", "d2_mfma", "d2_store"] if two else ["mfma", "store"]
             rep["tail"] = {nm: [round(float(np.median(us(t[:, tb + k + 1] - t[:, tb + k]))), 2),
                                 round(float(np.percentile(us(t[:, tb + k + 1] - t[:, tb + k]), 90)), 2)]
-                           for k, nm in enumerate(["mfma", "store"])}
-            rep["kernel_us"] = round(float(us(t[:, tb + 2].max() - start.min())), 2)
+                           for k, nm in enumerate(names)}
+            rep["kernel_us"] = round(float(us(t[:, tb + len(names)].max() - start.min())), 2)
     return rep
 
 
