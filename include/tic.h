@@ -111,8 +111,9 @@ int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out);
  * "chain" (each run of stride-1 64->64 layers in one launch; on for models 0-2, off for
  * model_3 / rmbe; declined automatically where the geometry cannot run it), "chain_wh"
  * (1 or 2), "chain_x" (1: the encoder's stride-2 layer in front of a run and the decoder's
- * transposed layer behind it run inside the chain's launch; needs chain_wh 2; default 0, the
- * shipped tuning decides), "chain_order" (region placement: 0 atomic ticket, 1 blockIdx, 2 a
+ * transposed layer behind it run inside the chain's launch; 2: also the decoder's next
+ * transposed layer (decode_2); needs chain_wh 2; default 1 for models 0-2, the shipped tuning
+ * decides), "chain_order" (region placement: 0 atomic ticket, 1 blockIdx, 2 a
  * patch's regions on one XCD, -1 automatic), "s1_form" (stride-1 form: 0 direct, 1 Winograd F(2x2,3x3), 2 Winograd F(4x4,3x3)
  * for the 64->64 res-block convs, other layers falling back to 1; -1 the model's default: 2 for
  * model_3 and the rmbe net, 1 otherwise; env TIC_S1_FORM=direct|wino|wino4), "decouple" (lanes fork from the
