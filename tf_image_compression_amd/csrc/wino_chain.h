@@ -125,6 +125,19 @@ __device__ __forceinline__ unsigned chain_region(unsigned b, unsigned R, unsigne
   return ((s / R) * 8 + x) * R + s % R;
 }
 
+// a - b on four floats as two packed adds with the second operand negated (v_pk_add_f32
+// neg_lo / neg_hi: each lane is the IEEE subtraction a + (-b), one rounding, the same value as
+// v_sub_f32), where hipcc lowers the vector subtraction to four unpacked v_sub_f32; at f32 the
+// VALU instructions beside the MFMAs add to the matrix time
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x4 psub(const f32x4 a, const f32x4 b) {
+  const f32x2 alo = {a.x, a.y}, ahi = {a.z, a.w}, blo = {b.x, b.y}, bhi = {b.z, b.w};
+  f32x2 lo, hi;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(lo) : "v"(alo), "v"(blo));
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(hi) : "v"(ahi), "v"(bhi));
+  return f32x4{lo.x, lo.y, hi.x, hi.y};
+}
+
 // 16-byte write-through (sc1) store / sc1 load through a buffer resource (aux 16 = sc1):
 // one buffer_store/load_dwordx4 instead of two 8-byte atomics (MI355X_MICROARCH.md: 8-B
 // accesses run at 0.54-0.70x the 16-B rate; hand-off table row 1 allows 16-B sc1 both sides)
@@ -511,18 +524,18 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       // VALU per 4-channel column
       if (sgn == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = d[0][j] - d[1][j];
+        for (int j = 0; j < 4; ++j) r[j] = psub(d[0][j], d[1][j]);
       } else if (sgn == 1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = d[0][j] + d[1][j];
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = d[1][j] - d[0][j];
+        for (int j = 0; j < 4; ++j) r[j] = psub(d[1][j], d[0][j]);
       }
-      V[0] = r[0] - r[2];
+      V[0] = psub(r[0], r[2]);
       V[1] = r[1] + r[2];
-      V[2] = r[2] - r[1];
-      V[3] = r[1] - r[3];
+      V[2] = psub(r[2], r[1]);
+      V[3] = psub(r[1], r[3]);
     };
     f32x4 acc[4][NBW];
 #pragma unroll
@@ -571,7 +584,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       const f32x4 m0 = acc[0][nb], m1 = acc[1][nb], m2 = acc[2][nb], m3 = acc[3][nb];
       float* x = &xch[(xi * 2 * NT + li) * XS + (wh * NBW + nb) * 16 + lg * 4];
       *reinterpret_cast<f32x4*>(x) = (m0 + m1) + m2;
-      *reinterpret_cast<f32x4*>(x + NT * XS) = (m1 - m2) - m3;
+      *reinterpret_cast<f32x4*>(x + NT * XS) = psub(psub(m1, m2), m3);
     }
     __syncthreads();
 
@@ -590,7 +603,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
 #pragma unroll
         for (int j = 0; j < 3; ++j)
           t[j] = *reinterpret_cast<const f32x4*>(&xch[(((ay + j) * 2 + b) * NT + et) * XS + 4 * eq]);
-        f32x4 v = ay == 0 ? (t[0] + t[1]) + t[2] : (t[0] - t[1]) - t[2];
+        f32x4 v = ay == 0 ? (t[0] + t[1]) + t[2] : psub(psub(t[0], t[1]), t[2]);
         v.x = __fadd_rn(v.x, bb.x);
         v.y = __fadd_rn(v.y, bb.y);
         v.z = __fadd_rn(v.z, bb.z);
