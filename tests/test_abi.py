@@ -234,3 +234,37 @@ def test_bench_dominant_by_kernel_family():
     assert abs(flops - 32 * (gs[0]["flops"] + gs[1]["flops"]) / 2) < 1e-3
     # two instances of another template are one family too (the template name up to '<')
     assert fams["conv3x3_kernel"]["launches"] == 2 and len(fams) == L - 10
+
+
+def test_bench_groups_chain_with_stride2_neighbours():
+    """With chain_x the encoder chain launch starts at encode_3 (its stride-2 head) and the
+    decoder chain launch ends with decode_3 and decode_2: one group each, whose FLOPs count the
+    Winograd form only for the stride-1 layers and the direct form for the stride-2 /
+    transposed ones (bench.kernel_groups), HBM bytes = the head's f32 input + the u8 symbols,
+    and the symbols + decode_2's f32 output."""
+    import importlib.util
+    import os
+    import numpy as np
+    from tf_image_compression_amd.topology import layer_table, layer_work
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    lt = layer_table(0)
+    names = [lay.name for lay in lt]
+    L = len(names)
+    kernels = [f"k{i}" for i in range(L)]
+    e3, d0, d2 = names.index("encode_3"), names.index("decode_4"), names.index("decode_2")
+    kernels[e3], kernels[d0] = "wino_chain_kernel<0,1,2,1>", "wino_chain_kernel<1,0,2,6>"
+    for i in list(range(e3 + 1, e3 + 6)) + list(range(d0 + 1, d2 + 1)):
+        kernels[i] = ""
+    groups, rows = bench.kernel_groups(None, 0, 256, np.full(L, 0.01), kernels)
+    enc = next(g for g in groups.values() if g["layers"][0] == "encode_3")
+    dec = next(g for g in groups.values() if g["layers"][0] == "decode_4")
+    assert enc["layers"][-1] == "encode_4" and dec["layers"][-1] == "decode_2"
+    work = layer_work(0, 256)
+    frac = lambda i: bench.WINO_FRAC if lt[i].kind == "conv_s1" else 1.0
+    assert enc["flops"] == sum(work[i][1] * frac(i) for i in range(e3, e3 + 6))
+    assert dec["flops"] == sum(work[i][1] * frac(i) for i in range(d0, d2 + 1))
+    assert rows[e3]["flops_per_patch"] == work[e3][1]  # the head: direct
+    assert enc["bytes"] == 32 * 32 * 64 * 4 + 16 * 16 * 64
+    assert dec["bytes"] == 16 * 16 * 64 + 64 * 64 * 32 * 4
