@@ -23,6 +23,8 @@ def main():
         import time
         if comm.rank == 1:
             time.sleep(float(os.environ.get("LATE_S", "3")))
+        if os.environ.get("LATE_AT") == "barrier":  # a per-step collective: the short default bound
+            comm.barrier()
         ok = dist.all_ranks(comm, comm.rank == 0)
         with open(f"{out}.{comm.rank}", "w") as f:
             json.dump({"rank": comm.rank, "all_ranks": ok, "all_true": dist.all_ranks(comm, True)}, f)

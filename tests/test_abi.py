@@ -268,3 +268,46 @@ def test_bench_groups_chain_with_stride2_neighbours():
     assert rows[e3]["flops_per_patch"] == work[e3][1]  # the head: direct
     assert enc["bytes"] == 32 * 32 * 64 * 4 + 16 * 16 * 64
     assert dec["bytes"] == 16 * 16 * 64 + 64 * 64 * 32 * 4
+
+
+def test_bench_direct_equiv_mixed_form_chain():
+    """roofline.direct_equiv_tflops of the chain family with its stride-2 head and transposed
+    tail: only the Winograd layers are converted to the direct form.  With
+    round 5's one-lane launch times (55.72 / 75.84 us per 32-patch launch) the direct-form
+    work (3.623 + 4.831 GFLOP) over 131.56 us is 64.3 TF/s, not the 87.2 that dividing the
+    whole group by 16/36 gave; `frac` stays on the executed (minimal-form) FLOPs."""
+    import importlib.util
+    import os
+    import numpy as np
+    from tf_image_compression_amd.topology import layer_table, layer_work
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    lt = layer_table(0)
+    names = {lay.name: i for i, lay in enumerate(lt)}
+    L = len(lt)
+    kernels = [f"k{i}" for i in range(L)]
+    e3, d0, d2 = names["encode_3"], names["decode_4"], names["decode_2"]
+    kernels[e3], kernels[d0] = "wino_chain_kernel<0,1,2,1>", "wino_chain_kernel<1,0,2,6>"
+    for i in list(range(e3 + 1, e3 + 6)) + list(range(d0 + 1, d2 + 1)):
+        kernels[i] = ""
+    ms = np.full(L, 0.001)
+    ms[e3], ms[d0] = 0.05572, 0.07584
+    groups, _ = bench.kernel_groups(None, 0, 256, ms, kernels)
+    fams = bench.kernel_families(groups, kernels, names)
+    fam = fams["wino_chain_kernel"]
+    work = layer_work(0, 256)
+    direct = sum(work[i][1] for i in range(e3, e3 + 6)) + sum(work[i][1] for i in range(d0, d2 + 1))
+    assert abs(fam["direct_flops"] * 2 - direct) < 1e-3
+    roof, dom_ms, dom_flops, _ = bench.roofline_of(fam, 32)
+    dom_k = sorted({kernels[names[nm]] for nm in fam["layers"]} - {""})
+    bench.winograd_note(roof, dom_k, fam, 32, dom_ms)
+    assert abs(direct * 32 / 1e9 - (3.623 + 4.831)) < 0.01
+    assert abs(roof["direct_equiv_tflops"] - 64.3) < 0.1, roof
+    assert "direct form for the stride-2" in roof["flop_form"]
+    assert abs(roof["frac"] - 0.2465) < 0.002  # executed FLOPs over the peak, unchanged
+    # a pure Winograd group keeps the plain 16/36 conversion
+    g = {"flops": 10e9 * bench.WINO_FRAC, "direct_flops": 10e9}
+    r = {}
+    bench.winograd_note(r, ["conv3x3_wino_kernel<64,64>"], g, 1, 1.0)
+    assert r["direct_equiv_tflops"] == 10.0 and "stride-2" not in r["flop_form"]

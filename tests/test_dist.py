@@ -157,6 +157,16 @@ def test_late_peer_within_collective_bound(tmp_path):
     assert [x["all_ranks"] for x in res] == [False, False] and all(x["all_true"] for x in res)
 
 
+def test_step_collective_keeps_short_bound(tmp_path):
+    """only collectives that follow rank-dependent work take the long bound (the
+    caller passes it; dist.all_ranks does); a per-step collective keeps the short default
+    (TIC_DIST_STEP_TIMEOUT), so a peer that stalls in the steady state ends the job quickly:
+    with the late arrival at a plain barrier and a 1 s step bound, rank 0 exits with code 3."""
+    r, _ = _run_late(tmp_path, {"TIC_DIST_STEP_TIMEOUT": "1", "LATE_AT": "barrier"})
+    assert r.returncode != 0
+    assert "gloo barrier did not complete within 1 s" in r.stderr
+
+
 def test_late_peer_beyond_collective_bound(tmp_path):
     """The same late arrival with the collective bound set under it: rank 0 ends with exit
     code 3 and names the wait instead of hanging."""

@@ -223,16 +223,22 @@ def test_wino_chain_stride2_neighbours_oversubscribed():
         assert all(np.array_equal(u8[i * 8:(i + 1) * 8], ref_u8) for i in range(64))
 
 
-@pytest.mark.parametrize("model_id,P,n", [(0, 256, 6), (0, 64, 5), (0, 48, 3), (1, 64, 4), (0, 288, 2)])
-def test_wino_chain_decode2_behind_tail_bit_identical(model_id, P, n):
+@pytest.mark.parametrize("model_id,P,n,fuse_tail", [(0, 256, 6, None), (0, 64, 5, None), (0, 48, 3, None),
+                                                    (1, 64, 4, None), (0, 288, 2, None), (2, 128, 4, 0)])
+def test_wino_chain_decode2_behind_tail_bit_identical(model_id, P, n, fuse_tail):
     """chain_x 2: decode_2 (transposed 64 -> 32) runs in the decoder chain's launch as well,
     on decode_3's output kept in LDS; decode_3's outputs just above / left of a region are
     recomputed from the run's halo ring in conv3x3_kernel's order (as dec10 does for decode_1),
     so everything stays bit-identical to the unfused launches: 2x2 regions (P = 256), one
     region (P = 64), one partial region (P = 48), 3x3 regions with partial ones at the bottom
-    and right (P = 288).  Reference layers: model_0/model.py:198-222 (decode_3, decode_2)."""
+    and right (P = 288).  model_2 with the decoder-tail fusion off: its decode_2 is
+    the layer before the network's last, so the chain's tail2 output feeds decode_1 (32 -> 3,
+    denorm, u8) running standalone.  Reference layers: model_0/model.py:198-222 (decode_3,
+    decode_2), model_2/model.py:190-235."""
     with _codec(model_id, P) as c:
         x = structured_patches(n, P, seed=770 + model_id + P)
+        if fuse_tail is not None:
+            c.set_option("fuse_tail", fuse_tail)
         c.set_option("s1_form", 1)
         c.set_option("chain", 0)
         ref = _run(c, x)

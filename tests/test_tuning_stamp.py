@@ -31,4 +31,6 @@ def test_tuning_stamp_matches_sources(path):
     text = doc["tuning"]
     assert text.startswith("tic-tuning 1\n")
     flags = {ln.split()[1] for ln in text.splitlines() if ln.startswith("flag ")}
-    assert {"fuse01", "fuse_tail", "s1_form", "chain", "chain_wh"} <= flags, flags
+    # chain_x too: tic_tuning_export always writes it, and without it a replay would fall back to
+    # the runtime default
+    assert {"fuse01", "fuse_tail", "s1_form", "chain", "chain_wh", "chain_x"} <= flags, flags

@@ -87,9 +87,13 @@ def env_rank() -> tuple[int, int, int]:
 
 # Bounds of the blocking waits (seconds).  Creating the communicator and the id rendezvous
 # happen right after every rank starts, so a short bound catches a missing peer early
-# (TIC_DIST_TIMEOUT).  A collective also waits for every peer to ARRIVE at it, and peers
-# arrive after rank-dependent work (tuning, measurement, an uneven shard), so collectives
-# get a bound sized for that work, not for the collective itself (TIC_DIST_COLLECTIVE_TIMEOUT).
+# (TIC_DIST_TIMEOUT).  A collective also waits for every peer to ARRIVE at it: a collective
+# that follows rank-dependent work (a tuning run on some ranks, rank 0's CPU baseline, an
+# uneven shard) gets a bound sized for that work — the caller passes
+# timeout=collective_timeout() (TIC_DIST_COLLECTIVE_TIMEOUT) — and every other collective
+# (the per-step ones: ranks arrive after the same work) keeps a short default bound,
+# step_timeout() (TIC_DIST_STEP_TIMEOUT, default the init bound), so a peer that dies in the
+# steady state ends the job in minutes, not half an hour.
 INIT_TIMEOUT = 150.0
 COLLECTIVE_TIMEOUT = 1800.0
 
@@ -99,7 +103,13 @@ def init_timeout() -> float:
 
 
 def collective_timeout() -> float:
+    """The bound of a collective that follows rank-dependent work (pass it explicitly)."""
     return float(os.environ.get("TIC_DIST_COLLECTIVE_TIMEOUT", COLLECTIVE_TIMEOUT))
+
+
+def step_timeout() -> float:
+    """The default bound of every other collective."""
+    return float(os.environ.get("TIC_DIST_STEP_TIMEOUT", init_timeout()))
 
 
 class Deadline:
@@ -142,7 +152,7 @@ class LocalComm:
     def allreduce_max(self, x: float, timeout: float | None = None) -> float:
         return float(x)
 
-    def allgather_stats(self, s: RankStats) -> list[RankStats]:
+    def allgather_stats(self, s: RankStats, timeout: float | None = None) -> list[RankStats]:
         return [s]
 
     def allgather_f64(self, a, timeout: float | None = None) -> np.ndarray:
@@ -165,7 +175,7 @@ class GlooComm:
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
 
     def _bound(self, what, timeout):
-        return Deadline(what, collective_timeout() if timeout is None else timeout, self.rank)
+        return Deadline(what, step_timeout() if timeout is None else timeout, self.rank)
 
     def barrier(self, timeout: float | None = None):
         with self._bound("gloo barrier", timeout):
@@ -178,8 +188,8 @@ class GlooComm:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
-    def allgather_stats(self, s: RankStats) -> list[RankStats]:
-        return [RankStats.from_array(r) for r in self.allgather_f64(s.to_array())]
+    def allgather_stats(self, s: RankStats, timeout: float | None = None) -> list[RankStats]:
+        return [RankStats.from_array(r) for r in self.allgather_f64(s.to_array(), timeout)]
 
     def allgather_f64(self, a, timeout: float | None = None) -> np.ndarray:
         import torch
@@ -297,7 +307,7 @@ class RcclComm:
 
     def allreduce_max(self, x: float, timeout: float | None = None) -> float:
         self.d_send.upload(np.array([x], np.float64))
-        with Deadline("ncclAllReduce(max)", collective_timeout() if timeout is None else timeout, self.rank):
+        with Deadline("ncclAllReduce(max)", step_timeout() if timeout is None else timeout, self.rank):
             self._ok(self.nccl.ncclAllReduce(self.d_send.ptr, self.d_recv.ptr, 1, NCCL_FLOAT64, NCCL_MAX, self.comm,
                                              self.stream), "ncclAllReduce")
             self.codec.synchronize()
@@ -312,14 +322,14 @@ class RcclComm:
         if a.size > self.cap:
             raise ValueError(f"allgather_f64 carries at most {self.cap} words per rank")
         self.d_send.upload(a)
-        with Deadline("ncclAllGather", collective_timeout() if timeout is None else timeout, self.rank):
+        with Deadline("ncclAllGather", step_timeout() if timeout is None else timeout, self.rank):
             self._ok(self.nccl.ncclAllGather(self.d_send.ptr, self.d_recv.ptr, a.size, NCCL_FLOAT64, self.comm,
                                              self.stream), "ncclAllGather")
             self.codec.synchronize()
         return self.d_recv.download((self.world, a.size), np.float64)
 
-    def allgather_stats(self, s: RankStats) -> list[RankStats]:
-        return [RankStats.from_array(r) for r in self.allgather_f64(s.to_array())]
+    def allgather_stats(self, s: RankStats, timeout: float | None = None) -> list[RankStats]:
+        return [RankStats.from_array(r) for r in self.allgather_f64(s.to_array(), timeout)]
 
     def close(self):
         if self.comm:
@@ -340,8 +350,9 @@ def make_comm(codec=None):
     return comm
 
 
-def all_ranks(comm, flag: bool) -> bool:
+def all_ranks(comm, flag: bool, timeout: float | None = None) -> bool:
     """True on every rank iff `flag` is true on every rank (one max-reduce of the negation):
     a decision every rank must take alike (e.g. whether to run the minutes-long tuning
-    before the first barrier) is taken from all ranks' inputs."""
-    return comm.allreduce_max(0.0 if flag else 1.0) == 0.0
+    before the first barrier) is taken from all ranks' inputs.  Ranks reach it after
+    rank-dependent work, so its bound is the collective one unless given."""
+    return comm.allreduce_max(0.0 if flag else 1.0, collective_timeout() if timeout is None else timeout) == 0.0

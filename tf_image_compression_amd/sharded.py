@@ -122,7 +122,7 @@ def run_device_shard(codec, comm, rank, world, n_images, batch=64, kind="structu
     shard = DeviceShard(codec, shard_images(n_images, rank, world, P, kind), batch)
     try:
         codec.synchronize()
-        comm.barrier()
+        comm.barrier(dist.collective_timeout())  # after building this rank's shard
         t0 = time.time()
         for _ in range(passes):
             shard.enqueue()
@@ -131,7 +131,7 @@ def run_device_shard(codec, comm, rank, world, n_images, batch=64, kind="structu
         st = shard.stats(passes, t0, t1)
     finally:
         shard.free()
-    return dist.combine(comm.allgather_stats(st)), st
+    return dist.combine(comm.allgather_stats(st, dist.collective_timeout())), st  # shards may be uneven
 
 
 def main(argv=None):
