@@ -40,6 +40,8 @@ def wino_frac(kernel):
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--tune-any-stamp", action="store_true",
+                    help="with an explicit --tune-cache file: replay it even when its stamp names other sources")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -691,6 +693,11 @@ def tune(args, codec, d_in, B, lane_b, M, P, search=True):
         if doc.get("_meta") == stamp:
             codec.tuning_import(doc["tuning"])
             return os.path.relpath(path, ROOT)
+        if args.tune_any_stamp and args.tune_cache not in ("auto", "none"):
+            # investigation runs (tools/kcounters.sh on candidate sources): the same launch plan
+            # replayed although its stamp names other sources — never the product's default
+            codec.tuning_import(doc["tuning"])
+            return os.path.relpath(path, ROOT) + " (replayed despite a stamp mismatch: --tune-any-stamp)"
     if not search:
         return "none (no replayable tuning; a shard smaller than one batch on some rank)"
     codec.autotune(d_in, lane_b, reps=5)  # per-layer tiling choice

@@ -256,3 +256,30 @@ def test_wino_chain_decode2_behind_tail_bit_identical(model_id, P, n, fuse_tail)
                 assert np.array_equal(a, b)
         c.set_option("chain_x", 1)
         assert not any(re.fullmatch(r"wino_chain_kernel<\d,\d,2,6>", k) for k in c.layer_kernels(n))
+
+
+def test_wino_chain_exact_fill_with_fewer_cus(monkeypatch):
+    """the automatic region order is the blockIdx-based, XCD-aware one (2) when
+    nlanes x n x R workgroups fit num_cus — model_0's shipped configuration sits exactly on that
+    line (2 lanes x 32 patches x 4 regions = 256).  A region under order 2 waits only on regions
+    of its own patch, dispatched to the same XCD right after it (blocks b, b+8, b+16, b+24), so
+    in-order dispatch per XCD needs R free slots per lane and XCD, not a slot for every
+    workgroup.  Checked here with the lane streams restricted to 248 of the CUs by a CU mask
+    (the grid of 256 chain workgroups cannot be resident at once): orders 2, 1 and 0 finish
+    without a hand-off timeout and bit-identical to the unfused path."""
+    monkeypatch.setenv("TIC_TEST_LANE_CU_OFF", "8")
+    P, n = 256, 64
+    x = structured_patches(n, P, seed=740)
+    with _codec(0, P) as c:
+        c.set_option("s1_form", 1)
+        c.set_option("streams", 2)
+        c.set_option("chain", 0)
+        ref = _run(c, x)
+        c.set_option("chain", 1)
+        c.set_option("chain_wh", 2)
+        for order in (-1, 2, 1, 0):
+            c.set_option("chain_order", order)
+            assert any("wino_chain" in k for k in c.layer_kernels(n // 2))
+            for _ in range(3):
+                got = _run(c, x)
+                assert all(np.array_equal(a, b) for a, b in zip(ref, got)), order

@@ -141,6 +141,10 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
   const int co_wave = wc * NB * 16;       // first channel of this wave inside the WG
 
   // ---- weight source ----
+#ifndef CONV_RSRC_STAGE
+#define CONV_RSRC_STAGE 1
+#endif
+  const __amdgpu_buffer_rsrc_t wrs_dma = weight_rsrc(a.wp, 9 * CIN * COUT * 4);
   auto wdma = [&](int tap, int slot) {  // LDS-DMA one tap slab: [kc][g][co_local][4]
 #pragma unroll
     for (int j = 0; j < (WCHUNK + 255) / 256; ++j) {
@@ -148,8 +152,14 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
       if (WCHUNK % 256 == 0 || cbase < WCHUNK) {
         const int c = cbase + lane;
         const int col = c % COUT_WG, kg = c / COUT_WG;  // kg = kc*4 + g
+#if CONV_RSRC_STAGE
+        // through the weights' buffer resource: 32-bit lane offset, the tap's offset in an SGPR
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs_dma, (lds_ptr_t)(smem + TILE + slot * WSLAB + cbase * 4), 16,
+                                                 ((kg * COUT + co_wg + col) * 4) * 4, tap * KC * 4 * COUT * 16, 0, 0);
+#else
         const float* src = a.wp + ((size_t)(tap * KC * 4 + kg) * COUT + co_wg + col) * 4;
         __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(smem + TILE + slot * WSLAB + cbase * 4), 16, 0, 0);
+#endif
       }
     }
   };
@@ -174,9 +184,20 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
 
   // ---- stage the input tile (with halo) into LDS; zero outside the image (SAME pad) ----
   // A thread's global loads are all issued before its first LDS write (batches of <= SB).
+  // f32 inputs go through a buffer resource over this patch (32-bit byte offsets; a position
+  // outside the image gets an offset past the resource's end, which the hardware reads as
+  // zero): no 64-bit address, zero-initialisation or branch per chunk — the staging VALU was
+  // ~60 % of encode_2's non-MFMA VALU (tools/isa_mix.py), and at f32 that VALU adds to the
+  // matrix time of the workgroups sharing the SIMD.  Patches of 4 GB or more
+  // (never at the shipped sizes) keep the pointer form.
   constexpr int NSTAGE = LR * LC * C4;
   constexpr int NIT = (NSTAGE + 255) / 256;
   constexpr int SB = NIT < 12 ? NIT : 12;
+  const size_t img_bytes = (size_t)H * W * CIN * 4;
+  const bool rsrc_in = CONV_RSRC_STAGE && IN == IN_F32 && img_bytes < 0xFFFFFF00ull;
+  const __amdgpu_buffer_rsrc_t irs =
+      weight_rsrc(reinterpret_cast<const float*>(a.in) + (rsrc_in ? (size_t)nimg * H * W * CIN : 0),
+                  (int)(unsigned)(rsrc_in ? img_bytes : 16));
 #pragma unroll
   for (int i0 = 0; i0 < NIT; i0 += SB) {
     f32x4 tmp[SB];
@@ -201,7 +222,11 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const ConvArgs a) {
           iy = gy0 - 1 + row;
           ix = gx0 - 1 + col;
         }
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        if (IN == IN_F32 && rsrc_in) {
+          const unsigned off = inside ? ((unsigned)(iy * W + ix) * CIN + c4 * 4) * 4u : 0xFFFFFFF0u;
+          tmp[i] = weight_frag(irs, (int)off, 0);
+        } else if (inside) {
           const size_t off = ((size_t)(nimg * H + iy) * W + ix) * CIN + c4 * 4;
           if constexpr (IN == IN_F32) {
             tmp[i] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.in) + off);
@@ -682,7 +707,8 @@ __global__ void __launch_bounds__(256) convT_rgb_scatter_kernel(const RgbOutArgs
 // CMP: the compact LDS form — layer 0's results are held in registers until every wave has
 // finished reading the RGB planes, then written into the layer-1 tile that aliases them;
 // that tile is unpadded (C0 floats per slot) with its 16-byte chunks XOR-swizzled per slot
-// (16 consecutive slots -> 16 distinct bank slots for ds_read_b128): 39 KB instead of 64 KB
+// (16 consecutive slots -> 16 distinct bank slots for ds_read_b128, 8 -> 8 for the stores):
+// 39 KB instead of 64 KB
 // at TH1 = 4, four workgroups per CU instead of two.  Bit-identical to the padded form.
 // ---------------------------------------------------------------------------------------
 template <int C0, int C1, int TH1, bool U8, bool CMP = false>
@@ -690,9 +716,21 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   static_assert(C0 % 16 == 0 && C1 % 16 == 0 && (TH1 % 4 == 0 || TH1 == 2), "tile");
   constexpr int R0 = 4 * TH1 + 3;        // RGB rows
   constexpr int QJ = 17;                 // entries per col%4 plane (67 cols -> 17)
-  constexpr int RGBP = R0 * 4 * QJ;      // floats per channel plane
+  // RGB row pitch (4 column planes of QJ, padded: 81 ≡ 17 mod 32, so the staging stores of two
+  // consecutive rows by one 32-lane half — 17 pixel groups a row — fill the 32 banks once) and
+  // channel-plane pitch (≡ 16 mod 32: the layer-0 gathers of lanes lg = 0 / 1 at one tap read two
+  // channels 16 banks apart): per instruction 2.0 -> 0.71 extra LDS cycles for the gathers,
+  // 2.25 -> 0 for the stores (tools/lds/enc01_banks.py)
+  constexpr int RP4 = 81;
+  static_assert(RP4 >= 4 * QJ, "row pitch");
+  constexpr int RGBP = R0 * RP4 + ((48 - (R0 * RP4) % 32) % 32);
   constexpr int LR1 = 2 * TH1 + 1, LC1 = 34, PS1 = CMP ? C0 : C0 + 8;
-  constexpr int NCH = C0 / 4, GRP = 16 / NCH;  // CMP swizzle: chunks per slot, slots per 256 B
+  // CMP swizzle: NCH chunks per slot; the key changes every GRP slots (GRP slots = 128 bytes):
+  // then the layer-1 operand reads (ds_read_b128, 16 consecutive slots at even AND odd slot
+  // offsets) and layer 0's result stores (ds_write_b128, 8 consecutive slots) are conflict-free —
+  // the key per 256 bytes (GRP = 16 / NCH) left the odd offsets' reads 3.1 and the stores 8
+  // extra cycles per instruction (tools/lds/enc01_banks.py)
+  constexpr int NCH = C0 / 4, GRP = 8 / NCH;
   constexpr int T1 = LR1 * LC1 * PS1;    // layer-1 input tile (floats)
   constexpr int NB0 = C0 / 16;
   constexpr int KC1 = C0 / 16;
@@ -748,7 +786,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
   const int ey0 = 2 * gy0 - a.pad1y, ex0 = 2 * gx0 - a.pad1x;   // first layer-0 pixel
   const int iy0 = 2 * ey0 - a.pad0y, ix0 = 2 * ex0 - a.pad0x;   // first RGB pixel
   auto put_rgb = [&](int rr, int col, int c, float x) {
-    rgb[c * RGBP + (rr * 4 + (col & 3)) * QJ + (col >> 2)] = __fdiv_rn(__fsub_rn(x, a.mean[c]), a.std[c]);
+    rgb[c * RGBP + rr * RP4 + (col & 3) * QJ + (col >> 2)] = __fdiv_rn(__fsub_rn(x, a.mean[c]), a.std[c]);
   };
   // zero the planes first where the tile leaves the image (SAME padding)
   const bool edge = iy0 < 0 || ix0 < 0 || iy0 + R0 > a.H || ix0 + 68 > a.W || !U8 || (ix0 * 3) % 4 != 0;
@@ -795,7 +833,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
         const int e = i * 256 + tid;
         if (e >= NG) break;
         const int rr = e / GPR, g = e % GPR;
-        float* const dst = rgb + rr * 4 * QJ + g;
+        float* const dst = rgb + rr * RP4 + g;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -815,7 +853,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           if constexpr (U8)
-            rgb[c * RGBP + (rr * 4 + (col & 3)) * QJ + (col >> 2)] =
+            rgb[c * RGBP + rr * RP4 + (col & 3) * QJ + (col >> 2)] =
                 lut[c * 256 + reinterpret_cast<const uint8_t*>(a.in)[off + c]];
           else
             put_rgb(rr, col, c, reinterpret_cast<const float*>(a.in)[off + c]);
@@ -837,7 +875,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
       bb[nb] = *reinterpret_cast<const f32x4*>(a.b0 + nb * 16 + lg * 4);
     }
     // per-lane LDS offsets of the 7 k-steps (k = 4t + lg -> channel, ky, kx), per column
-    // plane of the slot: offset = c*RGBP + ky*4*QJ + ((2 plane + kx) & 3)*QJ + ((2 plane + kx) >> 2)
+    // plane of the slot: offset = c*RGBP + ky*RP4 + ((2 plane + kx) & 3)*QJ + ((2 plane + kx) >> 2)
     int dl[2][7];
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
@@ -847,7 +885,7 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl) {
         const int q = 2 * pl + kx;
-        dl[pl][t] = k < 27 ? c * RGBP + ky * 4 * QJ + (q & 3) * QJ + (q >> 2) : -1;
+        dl[pl][t] = k < 27 ? c * RGBP + ky * RP4 + (q & 3) * QJ + (q >> 2) : -1;
       }
     }
     // Blocks of 16 slots: block 2r + p = tile row r, column plane p, j = 0..15 — a wave's
@@ -916,14 +954,14 @@ __global__ void __launch_bounds__(256, CMP ? (TH1 >= 8 ? 2 : 4) : 1) enc01_kerne
     // fixed and block jb adds a constant (the read's immediate offset)
     const float* gw[7];
 #pragma unroll
-    for (int t = 0; t < 7; ++t) gw[t] = rgb + (wave >> 1) * 8 * QJ + li + dw[t];
+    for (int t = 0; t < 7; ++t) gw[t] = rgb + (wave >> 1) * 2 * RP4 + li + dw[t];
     auto gather = [&](int jb, float (&b)[7]) {
       const int blk = wave + 4 * jb;
       if (blk < 2 * LR1) {  // wave-uniform
 #pragma unroll
-        for (int t = 0; t < 7; ++t) b[t] = gw[t][jb * 16 * QJ];
+        for (int t = 0; t < 7; ++t) b[t] = gw[t][jb * 4 * RP4];
       } else {
-        const int base = (lo_row(blk) < LR1 ? lo_row(blk) : 0) * 8 * QJ + 16;
+        const int base = (lo_row(blk) < LR1 ? lo_row(blk) : 0) * 2 * RP4 + 16;
 #pragma unroll
         for (int t = 0; t < 7; ++t) b[t] = rgb[base + dz[t]];
       }

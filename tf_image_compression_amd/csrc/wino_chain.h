@@ -43,6 +43,13 @@
 #pragma once
 #include "conv3x3_wino.h"
 
+#ifndef CH_D2_EARLY
+#define CH_D2_EARLY 0  // experiment: decode_2's phases stored as soon as their last tap is done
+#endif
+#ifndef CH_D2_PF
+#define CH_D2_PF 2     // decode_2's weight prefetch distance (steps)
+#endif
+
 namespace tic {
 
 constexpr int CH_MAX_LAYERS = 8;
@@ -50,8 +57,13 @@ constexpr int CH_MAX_LAYERS = 8;
 // epilogue done, border published, neighbours' flags seen, halo staged; then the head's six
 // (window staged, K loop done, epilogue done, published, flags seen, halo staged) and the
 // tail's (start, K loop done, stores issued)
-constexpr int CH_TS = 2 + 6 * (CH_MAX_LAYERS + 2);
+// tail's (start, K loop done, stores issued); then the same phase ends seen by wave 4 (the
+// second wave on SIMD 0: thread 0's phases also hold the wait for it) — per layer its K-loop
+// end, the head's and the tail's K-loop ends, decode_2's K-loop end and stores issued — and
+// the workgroup's end (after its last barrier)
 constexpr int CH_HEAD_TS = 2 + 6 * CH_MAX_LAYERS, CH_TAIL_TS = CH_HEAD_TS + 6;
+constexpr int CH_W4_TS = CH_TAIL_TS + 6, CH_W4_HEAD = CH_W4_TS + CH_MAX_LAYERS, CH_W4_TAIL = CH_W4_HEAD + 1;
+constexpr int CH_END_TS = CH_W4_TAIL + 3, CH_TS = CH_END_TS + 1;
 constexpr int CH_HEAD = 1, CH_TAIL = 2, CH_TAIL2 = 4;  // HT bits (CH_TAIL2 needs CH_TAIL)
 
 struct ChainLayer {
@@ -104,14 +116,29 @@ namespace chain {
 constexpr int C = 64, PS = 72, KC = 4;  // channels, LDS pixel stride (floats), 16-ch chunks
 constexpr int HP = 5, RP = 10, LR = 10; // parity half-row, row pitch (pixels), rows: 10x10 tile
 constexpr int NT = 16, TTX = 4;         // 2x2 tiles per region, tiles per tile row
-constexpr int XS = C + 8;               // T-exchange pitch
+constexpr int XS = C;                   // T-exchange pitch (16-byte chunks permuted: xq)
 constexpr int TILE = LR * RP * PS;      // 7200 floats
-constexpr int XCH = 8 * NT * XS;        // 9216 floats
+constexpr int XCH = 8 * NT * XS;        // 8192 floats
 constexpr int TB = TILE > XCH ? TILE : XCH;
 constexpr unsigned kSpinLimit = 1u << 19;  // ~0.5 s of polling before the error flag
 
 // LDS float offset of staged pixel (row, col) of a 10x10 tile (columns split by parity)
 __device__ __forceinline__ int tpix(int row, int col) { return (row * RP + (col & 1) * HP + (col >> 1)) * PS; }
+
+// LDS bank layout (MI355X_MICROARCH.md §LDS; model and search: tools/lds/chain_banks.py).
+// T exchange: channel quad q of tile `tile` sits in 16-byte chunk xq(tile, q) of the tile's
+// 256-byte row, so the K-loop waves' writes (8 consecutive tiles, one quad: 8 distinct bank
+// slots) and the epilogue's reads (below) are conflict-free — the 72-float pitch before made
+// them 2-way.
+__device__ __forceinline__ int xq(int tile, int q) { return (q + 2 * tile + ((tile >> 2) & 1)) & 15; }
+// Epilogue ownership: lane l of a wave takes tile 4 (wave % 4) + (l >> 4) and channel quad
+// (l - 2 (l >> 4)) mod 16 — with the tile's pixel pitch (18 chunks ≡ 2 mod 16) every 16-lane
+// read group of the residual / tile accesses then hits 16 distinct slots (quad = l mod 16 was
+// 2-way on the residual reads).
+__device__ __forceinline__ int epi_quad(int tid) { return ((tid & 15) - 2 * ((tid >> 4) & 3)) & 15; }
+// Stride-2 head / transposed tail: lane li of a wave owns region column dcol(li & 7) of its row
+// (bits 1 and 2 swapped): the tail's tile reads 4 -> 1.3 extra LDS cycles per instruction.
+__device__ __forceinline__ int dcol(int i) { return (i & 1) | ((i & 2) << 1) | ((i & 4) >> 1); }
 
 // Dispatch order 2: blocks b and b + 8 are dealt to one XCD (MI355X_MICROARCH.md), so block b
 // of a group of 8 R blocks takes region r of patch (group * 8 + b % 8) with r = (b / 8) % R:
@@ -187,6 +214,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   const int H = a.H, W = a.W, R = a.rh * a.rw, nR = a.n * R;
   auto stamp = [&](int k) {
     if (a.tstamp && tid == 0) a.tstamp[(size_t)blockIdx.x * CH_TS + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto stamp4 = [&](int k) {  // wave 4, the second wave on thread 0's SIMD (WH = 2)
+    if (a.tstamp && tid == 256) a.tstamp[(size_t)blockIdx.x * CH_TS + k] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
 
@@ -327,7 +357,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   // step order; wave w owns 16 output pixels (rows 2 (w % 4), +1 of the region: lane li ->
   // row (li >> 3), column li % 8) x output-channel blocks 2 (w / 4), +1 ----
   const int dnb = wv & 3, dmb = (wv >> 2) * 2;
-  const int dry = 2 * dnb + (li >> 3), drx = li & 7;  // this lane's pixel in the region
+  const int dry = 2 * dnb + (li >> 3), drx = dcol(li & 7);  // this lane's pixel in the region
   auto dsrc = [&](const float* w) { return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(w), (short)0, 9 * C * C * 4, 0x00020000); };
   auto dglob = [&](const __amdgpu_buffer_rsrc_t& r, int s, int m) -> f32x4 {
     const int tap = s / KC, kc = s % KC;  // step s: tap-major, then the 16-channel chunk
@@ -372,7 +402,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         const int e = i * NTH + tid;
         if (e < NCH) {
           const int c4 = e % 16, pe = e / 16, col = pe % 17, row = pe / 17;
-          *reinterpret_cast<f32x4*>(&hw[(row * HWC + (col & 1) * 9 + (col >> 1)) * PS + c4 * 4]) = tmp[i];
+          // chunk ^ 8 on row pairs 2, 3 (mod 4): the K loop's 16-lane groups read rows 2 apart
+          *reinterpret_cast<f32x4*>(&hw[(row * HWC + (col & 1) * 9 + (col >> 1)) * PS + (c4 ^ ((row & 2) << 2)) * 4]) =
+              tmp[i];
         }
       }
     }
@@ -381,8 +413,8 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     f32x4 dacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     auto hload = [&](int s) -> f32x4 {
       const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
-      const int pix = (2 * dry + ky) * HWC + (kx & 1) * 9 + drx + (kx >> 1);
-      return *reinterpret_cast<const f32x4*>(&hw[pix * PS + kc * 16 + lg * 4]);
+      const int row = 2 * dry + ky, pix = row * HWC + (kx & 1) * 9 + drx + (kx >> 1);
+      return *reinterpret_cast<const f32x4*>(&hw[pix * PS + ((kc * 4 + lg) ^ ((row & 2) << 2)) * 4]);
     };
     f32x4 bq[2];
     bq[0] = hload(0);
@@ -409,6 +441,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         for (int nb = 0; nb < NBW; ++nb) av[p][nb] = wglob(w0, p, nb);
     }
     stamp(CH_HEAD_TS + 1);
+    stamp4(CH_W4_HEAD);
     // + bias, ReLU (conv3x3_kernel's epilogue), into the block-input tile and the border record
     const __amdgpu_buffer_rsrc_t rpub = pub_rsrc(0);
     const bool in_img = oy0 + dry < H && ox0 + drx < W;
@@ -490,7 +523,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   const int offB = ((2 * ty_l + iB) * RP + tx_l) * PS + lg * 4;
   // epilogue ownership: one (tile, channel quad) per thread and output row ay (WH = 2:
   // the threads tid and tid + 256 take the tile's rows 0 and 1)
-  const int et = (tid & 255) >> 4, eq = tid & 15;
+  const int et = (tid & 255) >> 4, eq = epi_quad(tid);
   const int ay0 = WH == 1 ? 0 : tid >> 8;
   constexpr int nay = WH == 1 ? 2 : 1;
   const int ety = et / TTX, etx = et % TTX;
@@ -577,12 +610,13 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
     }
 
     stamp(ts + 1);
+    stamp4(CH_W4_TS + l);
     // ---- T = M A over nu, exchanged through LDS ----
     if (!SEPX) __syncthreads();  // every wave is done reading src (xch may alias it)
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const f32x4 m0 = acc[0][nb], m1 = acc[1][nb], m2 = acc[2][nb], m3 = acc[3][nb];
-      float* x = &xch[(xi * 2 * NT + li) * XS + (wh * NBW + nb) * 16 + lg * 4];
+      float* x = &xch[(xi * 2 * NT + li) * XS + xq(li, (wh * NBW + nb) * 4 + lg) * 4];
       *reinterpret_cast<f32x4*>(x) = (m0 + m1) + m2;
       *reinterpret_cast<f32x4*>(x + NT * XS) = psub(psub(m1, m2), m3);
     }
@@ -602,7 +636,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         f32x4 t[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          t[j] = *reinterpret_cast<const f32x4*>(&xch[(((ay + j) * 2 + b) * NT + et) * XS + 4 * eq]);
+          t[j] = *reinterpret_cast<const f32x4*>(&xch[(((ay + j) * 2 + b) * NT + et) * XS + xq(et, eq) * 4]);
         f32x4 v = ay == 0 ? (t[0] + t[1]) + t[2] : psub(psub(t[0], t[1]), t[2]);
         v.x = __fadd_rn(v.x, bb.x);
         v.y = __fadd_rn(v.y, bb.y);
@@ -711,6 +745,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       __builtin_amdgcn_sched_barrier(0);
     }
     stamp(CH_TAIL_TS + 1);
+    stamp4(CH_W4_TAIL);
     if constexpr (TAIL2) {
       // ---- decode_3's outputs stay on chip: they are decode_2's input tile T3 (17 x 17
       // positions, row / column 0 = the outputs just above / left of the region's 16 x 16).
@@ -747,6 +782,9 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       __syncthreads();  // every wave is done reading the run's tiles: T3 aliases them
       float* const t3 = smem;
       constexpr int T3C = 17, PS3 = PS;
+      // 16-byte chunk ch of T3 pixel (r, c) (chunk ^ 1 on columns 4-7 mod 8: decode_3's stride-2
+      // output writes were 4-way, now 2-way; decode_2's reads stay conflict-free)
+      auto t3a = [&](int r, int c, int ch) { return (r * T3C + c) * PS3 + (ch ^ ((c >> 2) & 1)) * 4; };
       auto epi = [&](f32x4 v, const f32x4& bb, bool valid) {
         v.x = __fadd_rn(v.x, bb.x);
         v.y = __fadd_rn(v.y, bb.y);
@@ -767,8 +805,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
           const int oy = 2 * dry + (p >> 1), ox = 2 * drx + (p & 1);
 #pragma unroll
           for (int m = 0; m < 2; ++m)
-            *reinterpret_cast<f32x4*>(&t3[((1 + oy) * T3C + 1 + ox) * PS3 + (dmb + m) * 16 + lg * 4]) =
-                epi(tacc[p][m], tbias[m], valid);
+            *reinterpret_cast<f32x4*>(&t3[t3a(1 + oy, 1 + ox, (dmb + m) * 4 + lg)]) = epi(tacc[p][m], tbias[m], valid);
         }
       }
       {  // the halo row / column (zero above / left of the image)
@@ -787,7 +824,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
             use = li < 8;
             valid = ox0 > 0 && oy0 + li < H;
           }
-          if (use) *reinterpret_cast<f32x4*>(&t3[(r * T3C + c) * PS3 + hm * 16 + lg * 4]) = epi(hacc[q], hb, valid);
+          if (use) *reinterpret_cast<f32x4*>(&t3[t3a(r, c, hm * 4 + lg)]) = epi(hacc[q], hb, valid);
         }
       }
       __syncthreads();
@@ -806,9 +843,10 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       f32x4 b2[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) b2[m] = *reinterpret_cast<const f32x4*>(a.tail2.bias + m * 16 + lg * 4);
-      f32x4 e2[DPF + 1][2];
+      constexpr int EPF = CH_D2_PF;
+      f32x4 e2[EPF + 1][2];
 #pragma unroll
-      for (int p = 0; p < DPF; ++p)
+      for (int p = 0; p < EPF; ++p)
 #pragma unroll
         for (int m = 0; m < 2; ++m) e2[p][m] = d2glob(p, m);
       f32x4 acc2[4][2][2];  // [phase][row of the wave][channel block]
@@ -822,39 +860,17 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         const int tap = s / KC, kc = s % KC, ky = tap / 3, kx = tap % 3;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          dst2[j] = *reinterpret_cast<const f32x4*>(
-              &t3[((1 + 2 * wv + j - (ky == 2)) * T3C + 1 + li - (kx == 2)) * PS3 + kc * 16 + lg * 4]);
+          dst2[j] = *reinterpret_cast<const f32x4*>(&t3[t3a(1 + 2 * wv + j - (ky == 2), 1 + li - (kx == 2), kc * 4 + lg)]);
       };
-      f32x4 bq2[2][2];
-      load2(0, bq2[0]);
-#pragma unroll
-      for (int s = 0; s < DSTEP; ++s) {
-        const int tap = s / KC, ky = tap / 3, kx = tap % 3;
-        const int ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
-        if (s + DPF < DSTEP) {
-#pragma unroll
-          for (int m = 0; m < 2; ++m) e2[(s + DPF) % (DPF + 1)][m] = d2glob(s + DPF, m);
-        }
-        if (s + 1 < DSTEP) load2(s + 1, bq2[(s + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-              acc2[ph][j][m] = mfma4(e2[s % (DPF + 1)][m][t], bq2[s & 1][j][t], acc2[ph][j][m]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      stamp(CH_TAIL_TS + 3);
-      // + bias, act; decode_2's output [n, 4H, 4W, 32], 16-byte stores
+      // + bias, act; decode_2's output [n, 4H, 4W, 32], 16-byte stores of phase p
       const int H3 = 2 * H, W3 = 2 * W, Ho2 = 4 * H, Wo2 = 4 * W;
+      auto store2 = [&](int p0, int p1) {  // phases p0 .. p1 - 1
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int gy = 2 * oy0 + 2 * wv + j, gx = 2 * ox0 + li;  // decode_2 input position
-        if (gy >= H3 || gx >= W3) continue;
+        for (int j = 0; j < 2; ++j) {
+          const int gy = 2 * oy0 + 2 * wv + j, gx = 2 * ox0 + li;  // decode_2 input position
+          if (gy >= H3 || gx >= W3) continue;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+          for (int p = p0; p < p1; ++p) {
           const int oy = 2 * gy + (p >> 1), ox = 2 * gx + (p & 1);
 #pragma unroll
           for (int m = 0; m < 2; ++m) {
@@ -872,9 +888,43 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
             }
             *reinterpret_cast<f32x4*>(a.tail2_out + ((size_t)(nimg * Ho2 + oy) * Wo2 + ox) * C2 + m * 16 + lg * 4) = v;
           }
+          }
+        }
+      };
+      f32x4 bq2[2][2];
+      load2(0, bq2[0]);
+#pragma unroll
+      for (int s = 0; s < DSTEP; ++s) {
+        const int tap = s / KC, ky = tap / 3, kx = tap % 3;
+        const int ph = (ky == 1 ? 2 : 0) + (kx == 1 ? 1 : 0);
+        if (s + EPF < DSTEP) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m) e2[(s + EPF) % (EPF + 1)][m] = d2glob(s + EPF, m);
+        }
+        if (s + 1 < DSTEP) load2(s + 1, bq2[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+              acc2[ph][j][m] = mfma4(e2[s % (EPF + 1)][m][t], bq2[s & 1][j][t], acc2[ph][j][m]);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (CH_D2_EARLY != 0) {
+          // a phase's last tap: 3 after tap 4, 2 after tap 5, 1 after tap 7 (the stores of the
+          // finished phases go out under the remaining taps' MFMAs; every output's sum is unchanged)
+          if (s == 4 * KC + KC - 1) store2(3, 4);
+          if (s == 5 * KC + KC - 1) store2(2, 3);
+          if (s == 7 * KC + KC - 1) store2(1, 2);
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
+      stamp(CH_TAIL_TS + 3);
+      stamp4(CH_W4_TAIL + 1);
+      store2(0, CH_D2_EARLY != 0 ? 1 : 4);
       stamp(CH_TAIL_TS + 4);
+      stamp4(CH_W4_TAIL + 2);
     } else {
     // + bias, act (conv3x3_kernel's epilogue), 16-byte f32 stores of the 16x16 output tile
     if (oy0 + dry < H && ox0 + drx < W) {
@@ -908,6 +958,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   // ---- the last workgroup to finish resets the ticket and advances the epoch ----
   if (failed) __hip_atomic_store(&a.ctl[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  stamp(CH_END_TS);
   if (tid == 0) {
     const unsigned done = __hip_atomic_fetch_add(&a.ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (done == gridDim.x - 1) {

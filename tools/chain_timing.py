@@ -71,6 +71,28 @@ def summarise(t, nl):
                                 round(float(np.percentile(us(t[:, tb + k + 1] - t[:, tb + k]), 90)), 2)]
                            for k, nm in enumerate(names)}
             rep["kernel_us"] = round(float(us(t[:, tb + len(names)].max() - start.min())), 2)
+    # round 6: the same phase ends seen by wave 4 (the second wave on thread 0's SIMD) and the
+    # workgroup's end (wino_chain.h CH_W4_TS .. CH_END_TS): "w4_lag" = how much later wave 4
+    # finishes a K loop than wave 0, i.e. how much of thread 0's next phase is its wait for it
+    w4 = hb + 12
+    if t.shape[1] >= w4 + 13:
+        med = lambda d: [round(float(np.median(us(d))), 2), round(float(np.percentile(us(d), 90)), 2)]
+        lag = {}
+        for l in range(nl):
+            if np.all(t[:, w4 + l] != 0):
+                lag[f"layer{l}"] = med(t[:, w4 + l] - t[:, 2 + 6 * l + 1])
+        if np.all(t[:, w4 + 8] != 0) and np.all(t[:, hb + 1] != 0):
+            lag["head"] = med(t[:, w4 + 8] - t[:, hb + 1])
+        tb = hb + 6
+        if np.all(t[:, w4 + 9] != 0):
+            lag["tail"] = med(t[:, w4 + 9] - t[:, tb + 1])
+        if np.all(t[:, w4 + 10] != 0):
+            lag["d2"] = med(t[:, w4 + 10] - t[:, tb + 3])
+            rep["w4_d2_store"] = med(t[:, w4 + 11] - t[:, w4 + 10])
+        rep["w4_lag"] = lag
+        if np.all(t[:, w4 + 12] != 0):
+            rep["wg_life_us"] = med(t[:, w4 + 12] - start)
+            rep["kernel_us"] = round(float(us(t[:, w4 + 12].max() - start.min())), 2)
     return rep
 
 

@@ -16,7 +16,7 @@ C="SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_IN
 for pass in a b c; do
   case $pass in a) CTR=$A ;; b) CTR=$B ;; c) CTR=$C ;; esac
   timeout -k 10 300 rocprofv3 --pmc $CTR --kernel-trace --output-format csv -d $O/pmc_$pass -o p -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 --tune-cache $TUNE --pmc-plan $O/plan_$pass.json "$@" \
+    python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 --tune-cache $TUNE --tune-any-stamp --pmc-plan $O/plan_$pass.json "$@" \
     > $O/$pass.log 2>&1
   rm -f $O/pmc_$pass/p_kernel_trace.csv
 done
