@@ -17,6 +17,7 @@ for part in "$@"; do
              tests/test_gpu_chain.py tests/test_gpu_product.py tests/test_gpu_parity.py ;;
     timing) step timing_$TAG 300 python tools/chain_timing.py --steps 40 ;;
     kc) step kc_$TAG 600 bash tools/kcounters.sh $TAG $T/model0_p256_b64_s2.json ;;
+    kc3) step kc3_$TAG 600 bash tools/kcounters.sh m3_$TAG $T/model3_p256_b256_s2.json --model 3 --batch 256 ;;
     kcold) TIC_LIB=$R/tf_image_compression_amd/libtic_old.so step kcold_$TAG 600 bash tools/kcounters.sh old_$TAG $T/model0_p256_b64_s2.json ;;
     ab) step ab_$TAG 900 bash tools/gpu_ab.sh $TAG 0 64 $T/model0_p256_b64_s2.json 4 ;;
     ab3) step ab3_$TAG 900 bash tools/gpu_ab.sh m3_$TAG 3 256 $T/model3_p256_b256_s2.json 3 ;;
@@ -24,6 +25,17 @@ for part in "$@"; do
              step abd2e_$TAG 900 bash tools/gpu_ab.sh d2e_$TAG 0 64 $T/model0_p256_b64_s2.json 3 ;;
     abd2e4) ABA=$R/tf_image_compression_amd/libtic.so ABB=$R/tf_image_compression_amd/libtic_d2e4.so \
              step abd2e4_$TAG 900 bash tools/gpu_ab.sh d2e4_$TAG 0 64 $T/model0_p256_b64_s2.json 3 ;;
+    abst) ABA=$R/tf_image_compression_amd/libtic_nostage.so step abst_$TAG 900 bash tools/gpu_ab.sh st_$TAG 0 64 \
+             $T/model0_p256_b64_s2.json 4 ;;
+    abst3) ABA=$R/tf_image_compression_amd/libtic_nostage.so step abst3_$TAG 900 bash tools/gpu_ab.sh st3_$TAG 3 256 \
+             $T/model3_p256_b256_s2.json 3 ;;
+    abpre) ABA=$R/tf_image_compression_amd/libtic_pre.so step abpre_$TAG 900 bash tools/gpu_ab.sh pre_$TAG 0 64 \
+             $T/model0_p256_b64_s2.json 4 ;;
+    abpre3) ABA=$R/tf_image_compression_amd/libtic_pre.so step abpre3_$TAG 900 bash tools/gpu_ab.sh pre3_$TAG 3 256 \
+             $T/model3_p256_b256_s2.json 3 ;;
+    abpfl) ABA=$R/tf_image_compression_amd/libtic.so ABB=$R/tf_image_compression_amd/libtic_pflate.so \
+             step abpfl_$TAG 900 bash tools/gpu_ab.sh pfl_$TAG 0 64 $T/model0_p256_b64_s2.json 4 ;;
+    timingv) TIC_LIB=$R/tf_image_compression_amd/libtic_$VAR.so step timing_${VAR}_$TAG 300 python tools/chain_timing.py --steps 40 ;;
     cumask) step cumask_$TAG 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
              tests/test_gpu_chain.py -k exact_fill ;;
     forms) step forms_layers_$TAG 300 python tools/layer_probe.py 0 32 'TIC_FUSE_TAIL=1' 'TIC_FUSE_TAIL=0' \
