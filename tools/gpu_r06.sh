@@ -48,7 +48,13 @@ for part in "$@"; do
              TIC_LANE_CU_SPLIT=half TIC_LANE_CU_SPLIT=alt ;;
     split3) step split3_$TAG 900 bash tools/gpu_ab_env.sh m3_$TAG 3 256 $T/model3_p256_b256_s2.json 3 - \
              TIC_LANE_CU_SPLIT=half TIC_LANE_CU_SPLIT=alt ;;
-    tune) step tune_m0_$TAG 600 python bench.py --tune-cache none --tune-save $R/gpurun_out/tune_$TAG \
+    tune) step tune_m0_$TAG 600 env TIC_TUNE_LOG=1 python bench.py --tune-cache none --tune-save $R/gpurun_out/tune_$TAG \
              --no-cpu-baseline --steps 50 --warmup 10 ;;
+    tune3) step tune_m3_$TAG 1000 env TIC_TUNE_LOG=1 python bench.py --model 3 --batch 256 --tune-cache none \
+             --tune-save $R/gpurun_out/tune_$TAG --no-cpu-baseline --steps 20 --warmup 5 ;;
+    tunec) step tune_c128_$TAG 600 env TIC_TUNE_LOG=1 python bench.py --model 128 --batch 64 --tune-cache none \
+             --tune-save $R/gpurun_out/tune_$TAG --no-cpu-baseline --steps 20 --warmup 5 ;;
+    tunei) step tune_img_$TAG 600 env TIC_TUNE_LOG=1 python bench.py --workload image4k --no-cpu-baseline --steps 10 \
+             --warmup 2 --tune-cache none --tune-save $R/gpurun_out/tune_$TAG ;;
   esac
 done
