@@ -621,11 +621,14 @@ int check_launch() {
 }
 
 // Time `nvar` launch variants (reps each, after one warm launch) and return the fastest.
-// Solo (one-lane) tuning picks among near-ties deterministically: the first candidate in the
-// fixed candidate order whose time is within kTieMargin of the fastest (VERDICT r05 item 7:
-// tilings 0.3 % apart flipped between boxes; a candidate now has to be 1.5 % faster than every
-// earlier one to be chosen, beyond the ±1 % run-to-run spread of relative timings)
-constexpr float kTieMargin = 0.015f;
+// Solo (one-lane) tuning picks among near-ties deterministically: every candidate is timed in
+// kSoloPasses round-robin passes (the median per candidate: one pass of a 15 µs kernel moved
+// by up to 5 % between runs), then the first candidate in the fixed candidate order whose
+// median is within kTieMargin of the fastest is chosen (two fresh tunings
+// on two boxes differed in one such pick; the whole-step tuner after it still switches a layer
+// when the step is confirmed faster)
+constexpr float kTieMargin = 0.03f;
+constexpr int kSoloPasses = 3;
 template <class T>
 static T pick_with_ties(const std::vector<std::pair<T, float>>& timed, T none) {
   float best = 1e30f;
@@ -634,6 +637,10 @@ static T pick_with_ties(const std::vector<std::pair<T, float>>& timed, T none) {
     if (c.second <= best * (1.f + kTieMargin)) return c.first;
   return none;
 }
+static float median_of(std::vector<float> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 1e30f : v[v.size() / 2];
+}
 
 int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(int)>& launch, int* best,
                   const char* label = "", int n = 0) {
@@ -641,18 +648,23 @@ int time_variants(hipStream_t st, int nvar, int reps, const std::function<bool(i
   Event t0, t1;
   HIP_TRY(t0.create());
   HIP_TRY(t1.create());
-  std::vector<std::pair<int, float>> timed;
-  for (int v = 0; v < nvar; ++v) {
-    if (!launch(v)) continue;
-    HIP_TRY(hipEventRecord(t0.e, st));
-    for (int r = 0; r < reps; ++r) launch(v);
-    HIP_TRY(hipEventRecord(t1.e, st));
-    HIP_TRY(hipEventSynchronize(t1.e));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, t0.e, t1.e));
-    if (log) fprintf(stderr, "tune %-22s n=%d variant %d : %.2f us\n", label, n, v, 1e3f * ms / reps);
-    timed.emplace_back(v, ms);
+  std::vector<std::vector<float>> samples(nvar);
+  for (int pass = 0; pass < kSoloPasses; ++pass) {
+    for (int v = 0; v < nvar; ++v) {
+      if (!launch(v)) continue;
+      HIP_TRY(hipEventRecord(t0.e, st));
+      for (int r = 0; r < reps; ++r) launch(v);
+      HIP_TRY(hipEventRecord(t1.e, st));
+      HIP_TRY(hipEventSynchronize(t1.e));
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, t0.e, t1.e));
+      if (log) fprintf(stderr, "tune %-22s n=%d variant %d : %.2f us\n", label, n, v, 1e3f * ms / reps);
+      samples[v].push_back(ms);
+    }
   }
+  std::vector<std::pair<int, float>> timed;
+  for (int v = 0; v < nvar; ++v)
+    if (!samples[v].empty()) timed.emplace_back(v, median_of(samples[v]));
   *best = pick_with_ties(timed, -1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(TIC_EHIP, "tuning launch failed: %s", hipGetErrorString(e));
@@ -1161,22 +1173,27 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         Event t0, t1;
         HIP_TRY(t0.create());
         HIP_TRY(t1.create());
-        std::vector<std::pair<const tic::ConvEntry*, float>> timed;
+        std::vector<std::vector<float>> samples(cands.size());
         const bool log = getenv("TIC_TUNE_LOG") != nullptr;
-        for (const tic::ConvEntry* c : cands) {
-          a.wp = conv_weights(lay, c);
-          c->fn(a, n, st);  // warm
-          HIP_TRY(hipEventRecord(t0.e, st));
-          for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, st);
-          HIP_TRY(hipEventRecord(t1.e, st));
-          HIP_TRY(hipEventSynchronize(t1.e));
-          float ms = 0.f;
-          HIP_TRY(hipEventElapsedTime(&ms, t0.e, t1.e));
-          if (log)
-            fprintf(stderr, "tune %-22s n=%d th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), n, c->th, c->nsplit,
-                    c->wlds, 1e3f * ms / h->tune_reps);
-          timed.emplace_back(c, ms);
+        for (int pass = 0; pass < kSoloPasses; ++pass) {
+          for (size_t ci = 0; ci < cands.size(); ++ci) {
+            const tic::ConvEntry* c = cands[ci];
+            a.wp = conv_weights(lay, c);
+            c->fn(a, n, st);  // warm
+            HIP_TRY(hipEventRecord(t0.e, st));
+            for (int r = 0; r < h->tune_reps; ++r) c->fn(a, n, st);
+            HIP_TRY(hipEventRecord(t1.e, st));
+            HIP_TRY(hipEventSynchronize(t1.e));
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, t0.e, t1.e));
+            if (log)
+              fprintf(stderr, "tune %-22s n=%d th=%d ns=%d w=%d : %.2f us\n", d.name.c_str(), n, c->th, c->nsplit,
+                      c->wlds, 1e3f * ms / h->tune_reps);
+            samples[ci].push_back(ms);
+          }
         }
+        std::vector<std::pair<const tic::ConvEntry*, float>> timed;
+        for (size_t ci = 0; ci < cands.size(); ++ci) timed.emplace_back(cands[ci], median_of(samples[ci]));
         if (!timed.empty()) e = pick_with_ties(timed, e);
         int rc = check_launch();
         if (rc) return rc;

@@ -36,6 +36,10 @@ for part in "$@"; do
     abpfl) ABA=$R/tf_image_compression_amd/libtic.so ABB=$R/tf_image_compression_amd/libtic_pflate.so \
              step abpfl_$TAG 900 bash tools/gpu_ab.sh pfl_$TAG 0 64 $T/model0_p256_b64_s2.json 4 ;;
     timingv) TIC_LIB=$R/tf_image_compression_amd/libtic_$VAR.so step timing_${VAR}_$TAG 300 python tools/chain_timing.py --steps 40 ;;
+    abtune) step abtune_$TAG 900 bash tools/gpu_ab_tune.sh m0_$TAG 0 64 $R/tools/tune_ab/model0_r05.json \
+             $T/model0_p256_b64_s2.json 5 ;;
+    abtune3) step abtune3_$TAG 900 bash tools/gpu_ab_tune.sh m3_$TAG 3 256 $R/tools/tune_ab/model3_r05.json \
+             $T/model3_p256_b256_s2.json 3 ;;
     cumask) step cumask_$TAG 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
              tests/test_gpu_chain.py -k exact_fill ;;
     forms) step forms_layers_$TAG 300 python tools/layer_probe.py 0 32 'TIC_FUSE_TAIL=1' 'TIC_FUSE_TAIL=0' \
