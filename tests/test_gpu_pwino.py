@@ -1,0 +1,121 @@
+"""GPU parity of the polyphase Winograd form of the stride-2 and transposed convs
+(conv3x3_pwino.h, handle option "s2_form" 1) against the CPU oracle.
+
+* per layer (the C-ABI's tic_conv3x3_device): max |gpu - oracle| <= 3e-5 * max(1, max|oracle|),
+  the same bar as the direct form, on even and odd sizes, partial tiles and workgroups, no
+  output left unwritten (reference ops: basic_block/basic_block.py:27-57 my_conv2d stride 2,
+  my_conv2d_transpose);
+* end to end: the codec bars of tests/gpu_checks.py for models 0, 2 and 3 with the form on;
+* the form never depends on a tuning: with s2_form 1 every bit-identical fusion switch
+  (fuse01, fuse_tail, chain, chain_x) still leaves every output bit unchanged, because the
+  layers those kernels could run keep the direct form (tic_runtime.cpp pwino_layer)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import structured_patches
+from gpu_checks import check_codec as _check_codec
+from oracle import tic_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+K_S2, K_T2 = 1, 2
+
+# (kind, cin, cout, act, NNB of the compiled instance)
+PWINO_LAYERS = [
+    (K_S2, 32, 64, 1, 1),
+    (K_S2, 64, 64, 1, 1),
+    (K_S2, 64, 128, 1, 1),
+    (K_T2, 64, 64, 1, 1),
+    (K_T2, 64, 32, 1, 2),
+    (K_T2, 64, 64, 0, 1),
+    (K_T2, 128, 64, 1, 1),
+]
+SIZES = [(32, 32), (17, 15), (5, 9), (70, 66), (1, 3)]
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    c = Codec(0, synthetic_params(0, seed=0), SYNTH_MEAN, SYNTH_STD, patch_size=64)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("kind,cin,cout,act,nnb", PWINO_LAYERS)
+def test_conv3x3_pwino_layer(codec, kind, cin, cout, act, nnb):
+    n = 2
+    for H, W in SIZES:
+        r = np.random.default_rng(np.random.PCG64(9100 + kind * 1000 + cin + cout + H * 7 + W))
+        x = r.standard_normal((n, H, W, cin)).astype(np.float32)
+        kshape = (3, 3, cout, cin) if kind == K_T2 else (3, 3, cin, cout)
+        k = (r.standard_normal(kshape) * np.sqrt(2.0 / (9 * cin))).astype(np.float32)
+        b = (r.standard_normal(cout) * 0.1).astype(np.float32)
+        params = {"l/kernel": k, "l/bias": b}
+        a = "relu" if act else "identity"
+        ref = o.my_conv2d_transpose(x, params, "l", a) if kind == K_T2 else o.my_conv2d(x, params, "l", 2, a)
+        d_in, d_out = codec.alloc(x.nbytes), codec.alloc(ref.nbytes)
+        try:
+            d_in.upload(x)
+            d_out.upload(np.full(ref.shape, np.nan, np.float32))
+            codec.set_option("s2_form", 1)
+            os.environ["TIC_FORCE_TILE"] = f"2,1,6,{nnb}"  # the polyphase instance, nothing else
+            codec.conv3x3_device(kind, act, d_in, n, H, W, cin, cout, k, b, None, d_out)
+            got = d_out.download(ref.shape, np.float32)
+        finally:
+            os.environ.pop("TIC_FORCE_TILE", None)
+            codec.set_option("s2_form", -1)
+            d_in.free()
+            d_out.free()
+        assert not np.isnan(got).any(), (H, W)
+        scale = max(1.0, float(np.max(np.abs(ref))))
+        err = float(np.max(np.abs(got - ref)))
+        assert err <= 3e-5 * scale, (H, W, err, scale)
+
+
+@pytest.mark.parametrize("model_id,P", [(0, 64), (2, 64), (3, 64), (0, 48)])
+def test_codec_s2_form_parity(model_id, P):
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    params = synthetic_params(model_id, seed=0)
+    with Codec(model_id, params, SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
+        patches = structured_patches(3, P, seed=910 + model_id + P)
+        c.set_option("s2_form", 1)
+        kern = c.layer_kernels(len(patches))
+        assert any(k.startswith("conv3x3_pwino_kernel") for k in kern), kern
+        _check_codec(c, params, model_id, P, patches)
+
+
+@pytest.mark.parametrize("model_id,P,n", [(0, 256, 4), (2, 128, 3), (3, 128, 2)])
+def test_s2_form_independent_of_fusions(model_id, P, n):
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    with Codec(model_id, synthetic_params(model_id, seed=0), SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
+        x = structured_patches(n, P, seed=930 + model_id)
+        c.set_option("s2_form", 1)
+
+        def run():
+            idx, pre = c.encode(x, return_preact=True)
+            u8, f = c.decode(idx, return_float=True)
+            return idx, pre, u8, f
+
+        states = [dict(fuse01=0, fuse_tail=0, chain=0), dict(fuse01=1, fuse_tail=1, chain=0)]
+        if model_id != 3:
+            states += [dict(fuse01=1, fuse_tail=1, chain=1, chain_wh=2, chain_x=1),
+                       dict(fuse01=1, fuse_tail=1, chain=1, chain_wh=2, chain_x=2)]
+        ref = None
+        for st in states:
+            for k, v in st.items():
+                c.set_option(k, v)
+            got = run()
+            if ref is None:
+                ref = got
+                continue
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b), st
+        # the standalone stride-2 layers outside every fused kernel do run the polyphase form
+        kern = c.layer_kernels(n)
+        assert any(re.match(r"conv3x3_pwino_kernel<[12],", k) for k in kern), kern

@@ -172,9 +172,10 @@ int same_pad(int kind, int h) {
 // workgroups.  `form` 1 selects the Winograd variants of stride-1 layers (weight source 4)
 // where compiled, 0 the direct ones.  TIC_FORCE_TILE="th,nsplit[,wsrc[,wr]]" overrides
 // (tuning experiments, tests); a forced weight source also overrides the form.
-// stride-1 form of a compiled entry: 1 Winograd F(2x2,3x3) (weight source 4), 2 Winograd
-// F(4x4,3x3) (weight source 5), else 0 (direct)
-int entry_form(const tic::ConvEntry& c) { return c.wlds == 4 ? 1 : (c.wlds == 5 ? 2 : 0); }
+// form of a compiled entry: stride-1 layers 1 Winograd F(2x2,3x3) (weight source 4), 2 Winograd
+// F(4x4,3x3) (weight source 5); stride-2 / transposed layers 1 polyphase Winograd (weight
+// source 6, conv3x3_pwino.h); else 0 (direct)
+int entry_form(const tic::ConvEntry& c) { return c.wlds == 4 || c.wlds == 6 ? 1 : (c.wlds == 5 ? 2 : 0); }
 
 // F(4x4,3x3) stages a patch through 32-bit buffer byte offsets: a patch (input or output) of
 // >= 2^29 floats cannot run in that form; every other entry fits any patch.
@@ -218,7 +219,9 @@ const tic::ConvEntry* find_conv(int mode, int cin, int cout, int act, int res, i
       // patches too large for F(4x4,3x3)'s 32-bit offsets run the next form (the codec's
       // 256x256 patches are far below)
       if (!wino4_fits(c, hg, wg)) continue;
-      const int cols = c.wlds == 4 ? 32 * c.wr / (c.th / 2) : (c.wlds == 5 ? 256 / c.th : 16);  // output columns / WG
+      const int cols = c.wlds == 4   ? 32 * c.wr / (c.th / 2)
+                       : c.wlds == 5 ? 256 / c.th
+                                     : (c.wlds == 6 ? 32 * c.wr : 16);  // columns of the grid per WG
       const long wgs = (long)((wg + cols - 1) / cols) * c.nsplit * ((hg + c.th - 1) / c.th) * std::max(n, 1);
       const long work = (long)c.th * cols * 4 / c.nsplit;  // pixels x channel-fraction per workgroup
       const bool ok = wgs >= 512;
@@ -325,6 +328,35 @@ void pack_wino4(const float* k, int cin, int cout, std::vector<float>* wp) {
     }
 }
 
+// Polyphase Winograd weights of a stride-2 conv (HWIO) or its transpose ([kh,kw,Cout,Cin]):
+// U = G g G^T per (ci, co) with G's rows the 1-D point weights of conv3x3_pwino.h
+// (stride 2: w0, w0 + w2, w2, w1, w1; transposed: W2, W2 + W0, W0, W1, W1), in double and
+// rounded once, packed [25 p = 5 xi + nu][Cin/16][4 g][Cout][4 t].
+void pack_pwino(const float* k, int kind, int cin, int cout, std::vector<float>* wp) {
+  static const double GS[5][3] = {{1, 0, 0}, {1, 0, 1}, {0, 0, 1}, {0, 1, 0}, {0, 1, 0}};
+  static const double GT[5][3] = {{0, 0, 1}, {1, 0, 1}, {1, 0, 0}, {0, 1, 0}, {0, 1, 0}};
+  const double(*G)[3] = kind == K_T2 ? GT : GS;
+  const int KC = cin / 16;
+  wp->assign((size_t)25 * cin * cout, 0.f);
+  for (int ci = 0; ci < cin; ++ci)
+    for (int co = 0; co < cout; ++co) {
+      double g[3][3];
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx) {
+          const int tap = ky * 3 + kx;
+          g[ky][kx] = kind == K_T2 ? k[((size_t)tap * cout + co) * cin + ci] : k[((size_t)tap * cin + ci) * cout + co];
+        }
+      const int kc = ci / 16, gg = (ci % 16) / 4, t = ci % 4;
+      for (int xi = 0; xi < 5; ++xi)
+        for (int nu = 0; nu < 5; ++nu) {
+          double u = 0;
+          for (int ky = 0; ky < 3; ++ky)
+            for (int kx = 0; kx < 3; ++kx) u += G[xi][ky] * g[ky][kx] * G[nu][kx];
+          (*wp)[((((size_t)(xi * 5 + nu) * KC + kc) * 4 + gg) * cout + co) * 4 + t] = (float)u;
+        }
+    }
+}
+
 // First layer: [Cout][4 g][8 t], k = 4t + g -> (tap, c) = divmod(k, 3); k = 27 -> 0.
 void pack_rgb_in(const float* k, int cout, std::vector<float>* wp) {
   wp->assign((size_t)cout * 32, 0.f);
@@ -386,6 +418,7 @@ struct LayerRT {
   float* d_w3 = nullptr;  // last layer: the TF kernel as-is (VALU form)
   float* d_ww = nullptr;  // stride-1 layers: Winograd-packed U (conv3x3_wino.h)
   float* d_ww4 = nullptr; // 64 -> 64 stride-1 layers: F(4x4,3x3) U (conv3x3_wino4.h)
+  float* d_wp = nullptr;  // stride-2 / transposed layers: polyphase Winograd U (conv3x3_pwino.h)
   float* d_b = nullptr;
   int h_in = 0, h_out = 0;  // spatial size for the handle's patch size
   std::map<int, const tic::ConvEntry*> tuned;  // batch size -> measured-best tiling
@@ -452,6 +485,8 @@ struct tic_handle {
   int persist_grid = 0;  // cap on persistent-kernel grids (0: CUs x resident workgroups); tests
   int wino4_max_n = 0;   // > 0: F(4x4,3x3) launches split into this many patches (tests of the split path)
   int s1_form = 0;       // stride-1 layers: 0 direct implicit GEMM, 1 Winograd F(2x2,3x3), 2 F(4x4,3x3)
+  int s2_form = 0;       // standalone stride-2 / transposed layers: 0 direct, 1 polyphase Winograd
+                         // (layers a fused kernel could run keep the direct form: pwino_layer)
   bool fuse_tail = false;  // decode_1 -> decode_0 through LDS (dec10_kernel; VALU last-layer form)
   bool chain = false;      // runs of stride-1 64->64 layers in one wino_chain_kernel launch (Winograd form)
   int chain_wh = 2;        // its workgroup: 1 = 256 threads, 2 = 512 (output channels split in halves)
@@ -494,14 +529,23 @@ struct tic_handle {
 // by the lanes' next fork: it may produce their inputs or still read their outputs.
 static void touch(tic_handle* h) { h->stream_dirty = true; }
 
-// Key of a layer's tuned-tiling map: the batch size, per stride-1 form (each form has its
-// own candidate set, so switching the form never reuses the other form's choice).
-static int tkey(const tic_handle* h, const LayerRT& l, int n) {
-  return l.def.kind == K_S1 && h->s1_form > 0 ? n + (h->s1_form << 24) : n;
+namespace {
+bool pwino_layer(const tic_handle* h, int i);
+}  // namespace
+// The form a standalone launch of this layer runs: the stride-1 policy for stride-1 layers;
+// for stride-2 / transposed layers the s2_form policy where pwino_layer allows it, else direct.
+static int layer_form(const tic_handle* h, const LayerRT& l) {
+  if (l.def.kind == K_S1) return h->s1_form;
+  return h->s2_form > 0 && pwino_layer(h, (int)(&l - h->layers.data())) ? h->s2_form : 0;
 }
-static int layer_form(const tic_handle* h, const LayerRT& l) { return l.def.kind == K_S1 ? h->s1_form : 0; }
+// Key of a layer's tuned-tiling map: the batch size, per form (each form has its own candidate
+// set, so switching the form never reuses the other form's choice).
+static int tkey(const tic_handle* h, const LayerRT& l, int n) {
+  const int f = layer_form(h, l);
+  return f > 0 ? n + (f << 24) : n;
+}
 static const float* conv_weights(const LayerRT& l, const tic::ConvEntry* e) {
-  return e->wlds == 4 ? l.d_ww : (e->wlds == 5 ? l.d_ww4 : l.d_w);
+  return e->wlds == 4 ? l.d_ww : (e->wlds == 5 ? l.d_ww4 : (e->wlds == 6 ? l.d_wp : l.d_w));
 }
 
 namespace {
@@ -704,6 +748,17 @@ int default_s1_form(int model_id) {
   return model_id == 3 || model_id == TIC_MODEL_RMBE ? 2 : 1;
 }
 
+// Stride-2 / transposed form policy: TIC_S2_FORM=direct|pwino, else built-in (see DESIGN.md §3
+// "polyphase Winograd"): the direct implicit GEMM until measured otherwise.
+int default_s2_form(int model_id) {
+  const char* f = getenv("TIC_S2_FORM");
+  const std::string s = f ? f : "";
+  if (s == "pwino") return 1;
+  if (s == "direct") return 0;
+  (void)model_id;
+  return 0;
+}
+
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
 // each form has its own summation order.  Default: the VALU form (variants 6-8);
 // TIC_RGB_OUT_FORM=dense (0-2) or scatter (3-5) for experiments and tests.  Tuning and
@@ -882,6 +937,38 @@ static bool any_chain_x(const tic_handle* h, int level = 1) {
   for (const ChainSpan& sp : chain_spans(h))
     if (level >= 2 ? sp.tail2 : (sp.head || sp.tail)) return true;
   return false;
+}
+
+// Whether stride-2 / transposed layer i may run the polyphase Winograd form (s2_form 1): only
+// where no fused kernel could run it under the handle's form policies — encode_1 (enc01),
+// decode_1 (dec10), and with the chain's stride-1 form (1) a chain's stride-2 head, transposed
+// tail and the decode_2 behind it keep the direct form (those kernels reproduce
+// conv3x3_kernel's order bit for bit).  The rule reads the topology and the form policies
+// only, never the tuned fusion flags, so a layer's results do not depend on a tuning.
+bool pwino_layer(const tic_handle* h, int i) {
+  const int L = (int)h->layers.size();
+  if (i <= 0 || i >= L - 1) return false;
+  const LayerDef& d = h->layers[i].def;
+  if (d.kind != K_S2 && d.kind != K_T2) return false;
+  const bool relu = d.act == 1 && !d.residual;
+  if (i == 1 && d.kind == K_S2 && relu && !(!h->rmbe() && h->n_enc == 2) &&
+      ((d.cin == 32 && d.cout == 32) || (d.cin == 16 && d.cout == 32) || (d.cin == 32 && d.cout == 64)))
+    return false;  // enc01's encode_1
+  if (i == L - 2 && d.kind == K_T2 && relu && rgb_out_form().lo == 6 && !(!h->rmbe() && L - 2 == h->n_enc) &&
+      ((d.cin == 32 && d.cout == 32) || (d.cin == 32 && d.cout == 16) || (d.cin == 64 && d.cout == 32)))
+    return false;  // dec10's decode_1
+  if (h->s1_form == 1) {
+    auto s1_64 = [&](int j) {
+      return j > 0 && j < L - 1 && h->layers[j].def.kind == K_S1 && h->layers[j].def.cin == 64 &&
+             h->layers[j].def.cout == 64;
+    };
+    if (s2_64_relu(d, K_S2) && s1_64(i + 1)) return false;  // a chain head
+    if (s2_64_relu(d, K_T2) && s1_64(i - 1)) return false;  // a chain tail
+    if (d.kind == K_T2 && d.cin == 64 && d.cout == 32 && relu && s2_64_relu(h->layers[i - 1].def, K_T2) &&
+        s1_64(i - 2))
+      return false;  // the decode_2 behind a tail
+  }
+  return true;
 }
 
 // Run layers [l0, l1) for n patches. Input: `in` (u8 patches, f32 windows or u8 symbols);
@@ -1444,6 +1531,7 @@ int tic_create(int model_id, int patch_size, int quan_scale, int device, tic_han
   if (const char* c = getenv("TIC_MAX_CHUNK")) h->chunk = std::max(1, atoi(c));
   if (const char* c = getenv("TIC_STREAMS")) h->nlanes = std::min(4, std::max(1, atoi(c)));
   h->s1_form = default_s1_form(model_id);
+  h->s2_form = default_s2_form(model_id);
   {
     const StructDefaults sd = struct_defaults(model_id);
     h->fuse01 = sd.fuse01;
@@ -1510,6 +1598,7 @@ void tic_destroy(tic_handle* h) {
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_ww4) (void)hipFree(l.d_ww4);
+    if (l.d_wp) (void)hipFree(l.d_wp);
     if (l.d_b) (void)hipFree(l.d_b);
   }
   clear_graphs(h);
@@ -1612,8 +1701,15 @@ int tic_finalize(tic_handle* h) {
     if (l.d_w3) (void)hipFree(l.d_w3);
     if (l.d_ww) (void)hipFree(l.d_ww);
     if (l.d_ww4) (void)hipFree(l.d_ww4);
+    if (l.d_wp) (void)hipFree(l.d_wp);
     if (l.d_b) (void)hipFree(l.d_b);
-    l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_ww4 = l.d_b = nullptr;
+    l.d_w = l.d_w2 = l.d_w3 = l.d_ww = l.d_ww4 = l.d_wp = l.d_b = nullptr;
+    if ((l.def.kind == K_S2 || l.def.kind == K_T2) && i > 0 && i < L - 1) {
+      std::vector<float> pw;
+      pack_pwino(l.k.data(), l.def.kind, l.def.cin, l.def.cout, &pw);
+      HIP_TRY(hipMalloc((void**)&l.d_wp, pw.size() * sizeof(float)));
+      HIP_TRY(hipMemcpy(l.d_wp, pw.data(), pw.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     if (l.def.kind == K_S1 && i > 0 && i < L - 1) {
       std::vector<float> ww;
       pack_wino(l.k.data(), l.def.cin, l.def.cout, &ww);
@@ -1886,6 +1982,13 @@ int tic_set_option(tic_handle* h, const char* key, int value) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     clear_graphs(h);
     h->s1_form = value < 0 ? default_s1_form(h->model_id) : value;
+    return TIC_OK;
+  }
+  if (k == "s2_form") {  // 0 direct, 1 polyphase Winograd, -1 the default (TIC_S2_FORM or built-in)
+    if (value < -1 || value > 1) return fail(TIC_EINVAL, "s2_form must be -1, 0 or 1");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    clear_graphs(h);
+    h->s2_form = value < 0 ? default_s2_form(h->model_id) : value;
     return TIC_OK;
   }
   return fail(TIC_EINVAL, "unknown option %s", key);
@@ -2476,7 +2579,10 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
             : find_conv(d.kind, d.cin, d.cout, d.act, d.residual, first_dec ? tic::IN_IDX : tic::IN_F32,
                                         last_enc ? tic::OUT_QUANT : tic::OUT_F32, hg, hg, n, layer_form(h, l));
     if (!e) return fail(TIC_EUNSUPPORTED, "layer %d has no compiled kernel", i);
-    if (e->wlds == 5)
+    if (e->wlds == 6)
+      snprintf(buf, sizeof buf, "conv3x3_pwino_kernel<%d,%d,%d,%d,%d,%s,%d,%d>", e->mode, e->cin, e->cout, e->wr,
+               e->act, tf[e->res != 0], e->in, e->out);
+    else if (e->wlds == 5)
       snprintf(buf, sizeof buf, "conv3x3_wino4_kernel<%d,%d,%d,%d,%s,%d,%d>", e->cin, e->cout, e->th / 4, e->act,
                tf[e->res != 0], e->in, e->out);
     else if (e->wlds == 4)
@@ -2500,6 +2606,7 @@ int tic_tuning_export(const tic_handle* h, char* buf, int cap) {
   t += "flag fuse01 " + std::to_string((int)h->fuse01) + "\n";
   t += "flag fuse_tail " + std::to_string((int)h->fuse_tail) + "\n";
   t += "flag s1_form " + std::to_string(h->s1_form) + "\n";
+  t += "flag s2_form " + std::to_string(h->s2_form) + "\n";
   t += "flag chain " + std::to_string((int)h->chain) + "\n";
   t += "flag chain_wh " + std::to_string(h->chain_wh) + "\n";
   t += "flag chain_x " + std::to_string((int)h->chain_x) + "\n";
@@ -2526,7 +2633,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   std::vector<std::map<int, const tic::ConvEntry*>> tuned(L);
   std::vector<std::map<int, int>> vars(L);
   int fuse01 = h->fuse01, fuse_tail = h->fuse_tail, s1_form = h->s1_form, chain = h->chain, chain_wh = h->chain_wh;
-  int chain_x = h->chain_x;
+  int chain_x = h->chain_x, s2_form = h->s2_form;
   const char* p = text;
   int line = 0;
   while (*p) {
@@ -2546,6 +2653,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
       if (!strcmp(name, "fuse01")) fuse01 = a != 0;
       else if (!strcmp(name, "fuse_tail")) fuse_tail = a != 0;
       else if (!strcmp(name, "s1_form") && a >= 0 && a <= 2) s1_form = a;
+      else if (!strcmp(name, "s2_form") && a >= 0 && a <= 1) s2_form = a;
       else if (!strcmp(name, "chain")) chain = a != 0;
       else if (!strcmp(name, "chain_wh") && a >= 1 && a <= 2) chain_wh = a;
       else if (!strcmp(name, "chain_x") && a >= 0 && a <= 2) chain_x = a;
@@ -2594,6 +2702,7 @@ int tic_tuning_import(tic_handle* h, const char* text) {
   h->fuse01 = fuse01;
   h->fuse_tail = fuse_tail;
   h->s1_form = s1_form;
+  h->s2_form = s2_form;
   h->chain = chain;
   h->chain_wh = chain_wh;
   h->chain_x = chain_x;
@@ -2609,13 +2718,14 @@ int tic_conv3x3_device(tic_handle* h, int kind, int act, const float* d_in, int 
   HIP_TRY(hipSetDevice(h->device));
   const tic::ConvEntry* e = find_conv(kind, cin, cout, act, d_res ? 1 : 0, tic::IN_F32, tic::OUT_F32,
                                       kind == K_T2 ? H : out_size(kind, H), kind == K_T2 ? W : out_size(kind, W), n,
-                                      kind == K_S1 ? h->s1_form : 0);
+                                      kind == K_S1 ? h->s1_form : h->s2_form);
   if (!e)
     return fail(TIC_EUNSUPPORTED, "no compiled conv3x3 for kind %d %d->%d act %d res %d", kind, cin, cout, act,
                 d_res ? 1 : 0);
   std::vector<float> wp;
   if (e->wlds == 4) pack_wino(w_host, cin, cout, &wp);
   else if (e->wlds == 5) pack_wino4(w_host, cin, cout, &wp);
+  else if (e->wlds == 6) pack_pwino(w_host, kind, cin, cout, &wp);
   else pack_generic(w_host, kind, cin, cout, &wp);
   Scratch s_w, s_b;
   HIP_TRY(s_w.alloc(wp.size() * 4));
