@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -31,11 +32,18 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E peak (spec)
 WINO_FRAC = 16.0 / 36.0
 # Winograd F(4x4,3x3) (s1_form 2, conv3x3_wino4_kernel): 36 points per 4x4 tile, 36/144 = 1/4
 WINO4_FRAC = 36.0 / 144.0
+# polyphase Winograd of the stride-2 / transposed convs (s2_form 1, conv3x3_pwino_kernel):
+# 25 points per tile against 36 products
+PWINO_FRAC = 25.0 / 36.0
 
 
-def wino_frac(kernel):
-    """Minimal-form share of the direct-form FLOPs for a layer run by `kernel`."""
-    return WINO4_FRAC if "wino4" in kernel else (WINO_FRAC if "wino" in kernel else 1.0)
+def wino_frac(kernel, kind="conv_s1"):
+    """Minimal-form share of the direct-form FLOPs for a layer of `kind` run by `kernel`
+    (Winograd forms of the stride-1 layers; a chain launch's stride-2 head / transposed tail
+    runs the direct form, the polyphase kernel the stride-2 / transposed layers)."""
+    if kind in ("conv_s1", "res"):
+        return WINO4_FRAC if "wino4" in kernel else (WINO_FRAC if "wino" in kernel else 1.0)
+    return PWINO_FRAC if "pwino" in kernel else 1.0
 
 
 def parse():
@@ -135,10 +143,13 @@ def kernel_groups(codec, model_id, P, ms, kernels=None):
         launch = []
         for k in kernels:
             launch.append(k if k or not launch else launch[-1])
-        # (Winograd forms run stride-1 layers only: a chain launch's stride-2 head / transposed
-        # tail is direct)
-        work = [(lay, f * (wino_frac(launch[i]) if lay.kind in ("conv_s1", "res") else 1.0), b, ho)
-                for i, (lay, f, b, ho) in enumerate(work)]
+        def form_kernel(i):
+            # a chain launch whose decode_2 behind the tail runs the polyphase form (HT bit 8,
+            # CH_TAIL2_PW): its last layer counts that form
+            m = re.match(r"wino_chain_kernel<\d+,\d+,\d+,(\d+)>", launch[i])
+            last = i + 1 >= len(kernels) or kernels[i + 1] != ""
+            return "pwino" if m and int(m.group(1)) & 8 and last else launch[i]
+        work = [(lay, f * wino_frac(form_kernel(i), lay.kind), b, ho) for i, (lay, f, b, ho) in enumerate(work)]
 
     def out_res_bytes(i):
         lay, _, _, ho = work[i]
@@ -241,12 +252,16 @@ def winograd_note(roof, kernels, group, batch, ms):
     only its Winograd layers: the equivalent rate is the group's direct-form FLOPs (every layer
     in the direct form, kernel_groups' `direct_flops`) over the launch time (VERDICT r05 item 6:
     dividing the whole group by 16/36 overstated it by 36 %)."""
-    if kernels and any("wino" in k for k in kernels):
+    if kernels and all("pwino" in k for k in kernels):
+        roof["flop_form"] = "polyphase winograd minimal form: 25/36 of the direct-form FLOPs"
+        roof["direct_equiv_tflops"] = round(group["direct_flops"] * batch / (ms * 1e-3) / 1e12, 2)
+    elif kernels and any("wino" in k for k in kernels):
         f4 = all("wino4" in k for k in kernels)
         form = ("winograd F(4x4,3x3) minimal form: 36/144 of the direct-form FLOPs" if f4 else
                 "winograd F(2x2,3x3) minimal form: 16/36 of the direct-form FLOPs")
         if abs(group["direct_flops"] * wino_frac(kernels[0]) - group["flops"]) > 1e-6 * group["flops"]:
-            form += " for the stride-1 layers; direct form for the stride-2 / transposed ones"
+            form += (" for the stride-1 layers; the stride-2 / transposed ones in their own form (direct, or"
+                     " polyphase winograd 25/36 where the s2_form policy runs it)")
         roof["flop_form"] = form
         roof["direct_equiv_tflops"] = round(group["direct_flops"] * batch / (ms * 1e-3) / 1e12, 2)
 

@@ -240,6 +240,7 @@ def test_wino_chain_decode2_behind_tail_bit_identical(model_id, P, n, fuse_tail)
         if fuse_tail is not None:
             c.set_option("fuse_tail", fuse_tail)
         c.set_option("s1_form", 1)
+        c.set_option("s2_form", 0)  # decode_2's direct form (the polyphase one: test_gpu_pwino.py)
         c.set_option("chain", 0)
         ref = _run(c, x)
         c.set_option("chain", 1)

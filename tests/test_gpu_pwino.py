@@ -119,3 +119,38 @@ def test_s2_form_independent_of_fusions(model_id, P, n):
         # the standalone stride-2 layers outside every fused kernel do run the polyphase form
         kern = c.layer_kernels(n)
         assert any(re.match(r"conv3x3_pwino_kernel<[12],", k) for k in kern), kern
+
+
+@pytest.mark.parametrize("model_id,P,n", [(0, 256, 6), (0, 64, 5), (0, 48, 3), (1, 64, 4), (0, 288, 2)])
+def test_chain_decode2_pwino_bit_identical(model_id, P, n):
+    """chain_x 2 with s2_form 1: the decode_2 behind the decoder chain's tail runs the
+    polyphase form inside the chain launch (HT bit CH_TAIL2_PW = 8) and matches the standalone
+    conv3x3_pwino_kernel bit for bit — 2x2 regions, one region, one partial region, 3x3 regions
+    with partial ones (P = 288), one and two lanes.  Reference: model_0/model.py:198-222."""
+    from tf_image_compression_amd.codec import Codec
+    from tf_image_compression_amd.weights import synthetic_params, SYNTH_MEAN, SYNTH_STD
+    with Codec(model_id, synthetic_params(model_id, seed=0), SYNTH_MEAN, SYNTH_STD, patch_size=P) as c:
+        x = structured_patches(n, P, seed=950 + model_id + P)
+        c.set_option("s1_form", 1)
+        c.set_option("s2_form", 1)
+        c.set_option("chain", 0)
+
+        def run():
+            idx, pre = c.encode(x, return_preact=True)
+            u8, f = c.decode(idx, return_float=True)
+            return idx, pre, u8, f
+
+        ref = run()
+        names = [lay[0] for lay in c.layers()]
+        assert c.layer_kernels(n)[names.index("decode_2")].startswith("conv3x3_pwino_kernel<2,64,32,")
+        c.set_option("chain", 1)
+        c.set_option("chain_wh", 2)
+        c.set_option("chain_x", 2)
+        for streams in (1, 2):
+            c.set_option("streams", streams)
+            kern = c.layer_kernels(n)
+            assert any(re.fullmatch(r"wino_chain_kernel<\d,\d,2,14>", k) for k in kern), kern
+            assert kern[names.index("decode_2")] == "", kern
+            got = run()
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b)

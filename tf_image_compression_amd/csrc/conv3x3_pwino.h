@@ -54,6 +54,42 @@ struct PwinoGeom {
   static constexpr int OPT = MODE == MODE_S2 ? 2 : 4;            // outputs per tile and axis
 };
 
+// The transforms, shared with the chain's decode_2 behind its tail (wino_chain.h), which must
+// reproduce this kernel bit for bit.  B^T over the NCOL values of one row / column:
+template <int MODE>
+__device__ __forceinline__ void pw_bt(const f32x4 (&r)[MODE == MODE_S2 ? 5 : 3], f32x4 (&v)[5]) {
+  if constexpr (MODE == MODE_S2) {
+    v[0] = r[0] - r[2];
+    v[1] = r[2];
+    v[2] = r[4] - r[2];
+    v[3] = r[1];
+    v[4] = r[3];
+  } else {
+    v[0] = r[0] - r[1];
+    v[1] = r[1];
+    v[2] = r[2] - r[1];
+    v[3] = r[1];
+    v[4] = r[2];
+  }
+}
+// transpose: row xi of B^T d from the tile's three input rows d0..d2 at column j
+__device__ __forceinline__ f32x4 pw_row_t2(int xi, const f32x4& d0, const f32x4& d1, const f32x4& d2) {
+  return xi == 0 ? d0 - d1 : (xi == 2 ? d2 - d1 : (xi == 4 ? d2 : d1));
+}
+// A^T over the five points of one row / column
+template <int MODE>
+__device__ __forceinline__ void pw_at(const f32x4 (&m)[5], f32x4 (&o)[MODE == MODE_S2 ? 2 : 4]) {
+  if constexpr (MODE == MODE_S2) {
+    o[0] = (m[0] + m[1]) + m[3];
+    o[1] = (m[1] + m[2]) + m[4];
+  } else {
+    o[0] = m[0] + m[1];
+    o[1] = m[3];
+    o[2] = m[1] + m[2];
+    o[3] = m[4];
+  }
+}
+
 // Weights (ConvArgs::wp): U packed [25 p = 5 xi + nu][Cin/16][4 g][Cout][4 t].
 // KS: the input channels are staged in KS slices (KS = 2 where the whole Cin would not leave
 // room for two workgroups per CU: the 64-channel stride-2 tiles), the K loop running over one
@@ -164,21 +200,7 @@ __global__ void __launch_bounds__(64 * (COUT / 16) * NNB) conv3x3_pwino_kernel(c
     return *reinterpret_cast<const f32x4*>(&smem[(row * RP + (j % NPL) * HP + t + j / NPL) * PS + kl * 16 + lg * 4]);
   };
   // B^T applied to the NCOL values of one row / column (exact: coefficients 0, +-1)
-  auto bt = [&](const f32x4 (&r)[NCOL], f32x4 (&v)[5]) {
-    if constexpr (MODE == MODE_S2) {
-      v[0] = r[0] - r[2];
-      v[1] = r[2];
-      v[2] = r[4] - r[2];
-      v[3] = r[1];
-      v[4] = r[3];
-    } else {
-      v[0] = r[0] - r[1];
-      v[1] = r[1];
-      v[2] = r[2] - r[1];
-      v[3] = r[1];
-      v[4] = r[2];
-    }
-  };
+  auto bt = [&](const f32x4 (&r)[NCOL], f32x4 (&v)[5]) { pw_bt<MODE>(r, v); };
 
   f32x4 acc[25];
 #pragma unroll
@@ -244,7 +266,7 @@ __global__ void __launch_bounds__(64 * (COUT / 16) * NNB) conv3x3_pwino_kernel(c
           f32x4 r[3], V[5];
 #pragma unroll
           for (int j = 0; j < 3; ++j)
-            r[j] = xi == 0 ? d[0][j] - d[1][j] : (xi == 2 ? d[2][j] - d[1][j] : (xi == 4 ? d[2][j] : d[1][j]));
+            r[j] = pw_row_t2(xi, d[0][j], d[1][j], d[2][j]);
           bt(r, V);
           row_mfma((h * KCS + kl) * 5 + xi, xi, V);
         }
@@ -256,17 +278,7 @@ __global__ void __launch_bounds__(64 * (COUT / 16) * NNB) conv3x3_pwino_kernel(c
   // ---- Y = A^T M A in registers (lane: tile t, output channels 16 cb + 4 lg .. + 3) ----
   // T[xi][b] = A over nu, then Y[a][b] = A over xi, in the orders written
   constexpr int O = G::OPT;
-  auto at = [&](const f32x4 (&m)[5], f32x4 (&o)[O]) {
-    if constexpr (MODE == MODE_S2) {
-      o[0] = (m[0] + m[1]) + m[3];
-      o[1] = (m[1] + m[2]) + m[4];
-    } else {
-      o[0] = m[0] + m[1];
-      o[1] = m[3];
-      o[2] = m[1] + m[2];
-      o[3] = m[4];
-    }
-  };
+  auto at = [&](const f32x4 (&m)[5], f32x4 (&o)[O]) { pw_at<MODE>(m, o); };
   f32x4 T[5][O];
 #pragma unroll
   for (int xi = 0; xi < 5; ++xi) {

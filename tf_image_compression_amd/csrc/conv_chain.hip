@@ -10,10 +10,10 @@ static bool launch_wh(int in_mode, int out_mode, const ChainArgs& a, hipStream_t
   const dim3 grid(a.n * a.rh * a.rw), block(256 * WH);
   if (in_mode == IN_F32 && out_mode == OUT_F32)
     hipLaunchKernelGGL((wino_chain_kernel<IN_F32, OUT_F32, WH, HT>), grid, block, 0, s, a);
-  else if (in_mode == IN_F32 && out_mode == OUT_QUANT && !(HT & (CH_TAIL | CH_TAIL2)))
+  else if (in_mode == IN_F32 && out_mode == OUT_QUANT && !(HT & (CH_TAIL | CH_TAIL2 | CH_TAIL2_PW)))
     hipLaunchKernelGGL((wino_chain_kernel<IN_F32, OUT_QUANT, WH, HT & CH_HEAD>), grid, block, 0, s, a);
   else if (in_mode == IN_IDX && out_mode == OUT_F32 && !(HT & CH_HEAD))
-    hipLaunchKernelGGL((wino_chain_kernel<IN_IDX, OUT_F32, WH, HT & (CH_TAIL | CH_TAIL2)>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((wino_chain_kernel<IN_IDX, OUT_F32, WH, HT & (CH_TAIL | CH_TAIL2 | CH_TAIL2_PW)>), grid, block, 0, s, a);
   else
     return false;
   return true;
@@ -30,6 +30,8 @@ bool launch_wino_chain(int in_mode, int out_mode, const ChainArgs& a, hipStream_
     if (ht == CH_HEAD) return launch_wh<2, CH_HEAD>(in_mode, out_mode, a, s);
     if (ht == CH_TAIL) return launch_wh<2, CH_TAIL>(in_mode, out_mode, a, s);
     if (ht == (CH_TAIL | CH_TAIL2)) return launch_wh<2, CH_TAIL | CH_TAIL2>(in_mode, out_mode, a, s);
+    if (ht == (CH_TAIL | CH_TAIL2 | CH_TAIL2_PW))
+      return launch_wh<2, CH_TAIL | CH_TAIL2 | CH_TAIL2_PW>(in_mode, out_mode, a, s);
     return false;
   }
   if (wh == 1) return launch_wh<1, 0>(in_mode, out_mode, a, s);

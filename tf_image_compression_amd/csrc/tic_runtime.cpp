@@ -748,15 +748,19 @@ int default_s1_form(int model_id) {
   return model_id == 3 || model_id == TIC_MODEL_RMBE ? 2 : 1;
 }
 
-// Stride-2 / transposed form policy: TIC_S2_FORM=direct|pwino, else built-in (see DESIGN.md §3
-// "polyphase Winograd"): the direct implicit GEMM until measured otherwise.
+// Stride-2 / transposed form policy: TIC_S2_FORM=direct|pwino, else built-in (DESIGN.md §3
+// "polyphase Winograd"): the polyphase form for models 0/1, whose layers it runs (encode_2, a
+// 64x64 -> 32x32 grid of 512+ workgroups per lane, and the decode_2 behind the decoder chain's
+// tail) got faster with it (model_0 configs[1] step -1.3 / -1.8 % in two alternating A/B runs);
+// the direct form elsewhere: model_2's encode_4 / decode_4, model_3's 64- and 80-channel layers
+// and the rmbe / ch_128 layers measured slower in it (one workgroup per CU or 2.8x the weight
+// bytes per output of the direct form, profiles/ab_r06_pwino.json).
 int default_s2_form(int model_id) {
   const char* f = getenv("TIC_S2_FORM");
   const std::string s = f ? f : "";
   if (s == "pwino") return 1;
   if (s == "direct") return 0;
-  (void)model_id;
-  return 0;
+  return model_id == 0 || model_id == 1 ? 1 : 0;
 }
 
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
@@ -941,10 +945,12 @@ static bool any_chain_x(const tic_handle* h, int level = 1) {
 
 // Whether stride-2 / transposed layer i may run the polyphase Winograd form (s2_form 1): only
 // where no fused kernel could run it under the handle's form policies — encode_1 (enc01),
-// decode_1 (dec10), and with the chain's stride-1 form (1) a chain's stride-2 head, transposed
-// tail and the decode_2 behind it keep the direct form (those kernels reproduce
-// conv3x3_kernel's order bit for bit).  The rule reads the topology and the form policies
-// only, never the tuned fusion flags, so a layer's results do not depend on a tuning.
+// decode_1 (dec10), and with the chain's stride-1 form (1) a chain's stride-2 head and
+// transposed tail keep the direct form (those kernels reproduce conv3x3_kernel's order bit for
+// bit); the decode_2 a chain can run behind its tail has both forms in the chain kernel
+// (CH_TAIL2_PW reproduces conv3x3_pwino_kernel), so it follows the policy.  The rule reads
+// the topology and the form policies only, never the tuned fusion flags, so a layer's results
+// do not depend on a tuning.
 bool pwino_layer(const tic_handle* h, int i) {
   const int L = (int)h->layers.size();
   if (i <= 0 || i >= L - 1) return false;
@@ -964,9 +970,6 @@ bool pwino_layer(const tic_handle* h, int i) {
     };
     if (s2_64_relu(d, K_S2) && s1_64(i + 1)) return false;  // a chain head
     if (s2_64_relu(d, K_T2) && s1_64(i - 1)) return false;  // a chain tail
-    if (d.kind == K_T2 && d.cin == 64 && d.cout == 32 && relu && s2_64_relu(h->layers[i - 1].def, K_T2) &&
-        s1_64(i - 2))
-      return false;  // the decode_2 behind a tail
   }
   return true;
 }
@@ -1145,9 +1148,11 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         a.tail = {tl.d_w, tl.d_b, tl.def.act, 0};
         a.tail_out = ws[dst];
       }
-      if (sp.tail2) {  // and the next one (decode_2), whose output is the next activation instead
+      const bool tail2_pw = sp.tail2 && layer_form(h, h->layers[ce + 1]) == 1;
+      if (sp.tail2) {  // and the next one (decode_2), whose output is the next activation instead;
+                       // in its polyphase Winograd form where the s2_form policy runs it so
         const LayerRT& tl2 = h->layers[ce + 1];
-        a.tail2 = {tl2.d_w, tl2.d_b, tl2.def.act, 0};
+        a.tail2 = {tail2_pw ? tl2.d_wp : tl2.d_w, tl2.d_b, tl2.def.act, 0};
         a.tail2_out = ws[dst];
       }
       if (const char* pr = getenv("TIC_CHAIN_PROBE")) a.probe = atoi(pr);
@@ -1156,7 +1161,8 @@ int run_layers(tic_handle* h, Lane& ln, int l0, int l1, const void* in, int n, u
         if (rc2) return rc2;
       }
       const int inm = first_dec_c ? tic::IN_IDX : tic::IN_F32, outm = last_enc_c ? tic::OUT_QUANT : tic::OUT_F32;
-      const int ht = (sp.head ? tic::CH_HEAD : 0) | (sp.tail ? tic::CH_TAIL : 0) | (sp.tail2 ? tic::CH_TAIL2 : 0);
+      const int ht = (sp.head ? tic::CH_HEAD : 0) | (sp.tail ? tic::CH_TAIL : 0) | (sp.tail2 ? tic::CH_TAIL2 : 0) |
+                     (tail2_pw ? tic::CH_TAIL2_PW : 0);
       if (!tic::launch_wino_chain(inm, outm, a, st, h->chain_wh, ht))
         return fail(TIC_EUNSUPPORTED, "no chain kernel for layers %d..%d", li, sp.last());
       rc = check_launch();
@@ -2536,7 +2542,8 @@ int tic_layer_kernel(const tic_handle* h, int i, int n, char* name, int cap) {
   if (cs.valid()) {
     if (cs.start == i) {
       const bool first_dec = !h->rmbe() && cs.s1 == h->n_enc, last_enc = !h->rmbe() && cs.end - 1 == h->n_enc - 1;
-      const int ht = (cs.head ? tic::CH_HEAD : 0) | (cs.tail ? tic::CH_TAIL : 0) | (cs.tail2 ? tic::CH_TAIL2 : 0);
+      const int ht = (cs.head ? tic::CH_HEAD : 0) | (cs.tail ? tic::CH_TAIL : 0) | (cs.tail2 ? tic::CH_TAIL2 : 0) |
+                     (cs.tail2 && layer_form(h, h->layers[cs.end + 1]) == 1 ? tic::CH_TAIL2_PW : 0);
       snprintf(buf, sizeof buf, "wino_chain_kernel<%d,%d,%d,%d>", first_dec ? 1 : 0, last_enc ? 1 : 0, h->chain_wh,
                ht);
     }

@@ -41,7 +41,7 @@
 // the 16x16 output tile of its region.  Both are bit-identical to the standalone launches
 // (tests/test_gpu_chain.py); they remove two launches per lane and their HBM round trips.
 #pragma once
-#include "conv3x3_wino.h"
+#include "conv3x3_pwino.h"
 
 #ifndef CH_D2_EARLY
 #define CH_D2_EARLY 0  // experiment: decode_2's phases stored as soon as their last tap is done
@@ -65,6 +65,8 @@ constexpr int CH_HEAD_TS = 2 + 6 * CH_MAX_LAYERS, CH_TAIL_TS = CH_HEAD_TS + 6;
 constexpr int CH_W4_TS = CH_TAIL_TS + 6, CH_W4_HEAD = CH_W4_TS + CH_MAX_LAYERS, CH_W4_TAIL = CH_W4_HEAD + 1;
 constexpr int CH_END_TS = CH_W4_TAIL + 3, CH_TS = CH_END_TS + 1;
 constexpr int CH_HEAD = 1, CH_TAIL = 2, CH_TAIL2 = 4;  // HT bits (CH_TAIL2 needs CH_TAIL)
+// decode_2 behind the tail in the polyphase Winograd form (s2_form 1; needs CH_TAIL2)
+constexpr int CH_TAIL2_PW = 8;
 
 struct ChainLayer {
   const float* wu;    // Winograd U [16 p][4 kc][4 g][64][4 t] (pack_wino)
@@ -193,6 +195,8 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
   using namespace chain;
   constexpr int NTH = 256 * WH;
   constexpr bool HEAD = (HT & CH_HEAD) != 0, TAIL = (HT & CH_TAIL) != 0, TAIL2 = (HT & CH_TAIL2) != 0;
+  constexpr bool TAIL2_PW = (HT & CH_TAIL2_PW) != 0;
+  static_assert(!TAIL2_PW || TAIL2, "the polyphase decode_2 is the one behind the tail");
   static_assert(!TAIL2 || TAIL, "decode_2 runs on the tail's output");
   static_assert(HT == 0 || WH == 2, "stride-2 head / tail: 512-thread workgroups only");
   // WH = 2 (one workgroup per CU): the T exchange gets a buffer of its own beside the two
@@ -829,6 +833,102 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       }
       __syncthreads();
       stamp(CH_TAIL_TS + 2);
+      if constexpr (TAIL2_PW) {
+        // ---- decode_2 in the polyphase Winograd form (s2_form 1), conv3x3_pwino_kernel<MODE_T2,
+        // 64, 32>'s arithmetic bit for bit (the same pw_* transforms, every point summed over the
+        // chunks and t in the same order, the same output transform and epilogue): tile (ty, tx)
+        // = decode_2 input positions 2ty .. 2ty + 1 x 2tx .. 2tx + 1 of the region's 16 x 16,
+        // reading T3 positions (2ty + r, 2tx + j), r, j = 0..2 (row / column 0: the halo); wave w
+        // owns output-channel block w & 1 and tile rows 2 (w >> 1) .. + 1 (lane li: tile
+        // (2 (w >> 1) + li / 8, li % 8)), all 25 points: 400 MFMAs per wave instead of 576 ----
+        constexpr int C2 = 32, PPF = 8, PSTEP = 25 * KC;
+        const int pcb = wv & 1, pty = 2 * (wv >> 1) + (li >> 3), ptx = li & 7;
+        const __amdgpu_buffer_rsrc_t w2s =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.tail2.wu), (short)0, 25 * C * C2 * 4, 0x00020000);
+        auto pwglob = [&](int s) -> f32x4 {  // step s = 25 kc + 5 xi + nu (pack_pwino's layout)
+          const int kc = s / 25, p = s % 25;
+          const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(w2s, (lg * C2 + pcb * 16 + li) * 16,
+                                                                ((p * KC + kc) * 4 * C2 * 4) * 4, 0);
+          return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
+        };
+        f32x4 pav[PPF + 1];
+#pragma unroll
+        for (int p = 0; p < PPF; ++p) pav[p] = pwglob(p);
+        const f32x4 pb = *reinterpret_cast<const f32x4*>(a.tail2.bias + pcb * 16 + lg * 4);
+        f32x4 pacc[25];
+#pragma unroll
+        for (int p = 0; p < 25; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 db[2][3][3];
+        auto ldchunk = [&](int kc, f32x4 (&dst)[3][3]) {
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+              dst[r][j] = *reinterpret_cast<const f32x4*>(&t3[t3a(2 * pty + r, 2 * ptx + j, kc * 4 + lg)]);
+        };
+        ldchunk(0, db[0]);
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          if (kc + 1 < KC) ldchunk(kc + 1, db[(kc + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          const f32x4(&d)[3][3] = db[kc & 1];
+#pragma unroll
+          for (int xi = 0; xi < 5; ++xi) {
+            f32x4 r[3], V[5];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) r[j] = pw_row_t2(xi, d[0][j], d[1][j], d[2][j]);
+            pw_bt<MODE_T2>(r, V);
+#pragma unroll
+            for (int nu = 0; nu < 5; ++nu) {
+              const int s = 25 * kc + 5 * xi + nu;
+              if (s + PPF < PSTEP) pav[(s + PPF) % (PPF + 1)] = pwglob(s + PPF);
+              const f32x4 u = pav[s % (PPF + 1)];
+#pragma unroll
+              for (int tt = 0; tt < 4; ++tt) pacc[5 * xi + nu] = mfma4(u[tt], V[nu][tt], pacc[5 * xi + nu]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        stamp(CH_TAIL_TS + 3);
+        stamp4(CH_W4_TAIL + 1);
+        // Y = A^T M A, + bias, act, 16-byte stores of the tile's 4 x 4 outputs
+        f32x4 T[5][4];
+#pragma unroll
+        for (int xi = 0; xi < 5; ++xi) {
+          f32x4 m[5];
+#pragma unroll
+          for (int nu = 0; nu < 5; ++nu) m[nu] = pacc[5 * xi + nu];
+          pw_at<MODE_T2>(m, T[xi]);
+        }
+        const int Ho2 = 4 * H, Wo2 = 4 * W;
+        const int py0 = 4 * oy0 + 4 * pty, px0 = 4 * ox0 + 4 * ptx;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          f32x4 m[5], y[4];
+#pragma unroll
+          for (int xi = 0; xi < 5; ++xi) m[xi] = T[xi][b];
+          pw_at<MODE_T2>(m, y);
+#pragma unroll
+          for (int ay = 0; ay < 4; ++ay) {
+            const int oy = py0 + ay, ox = px0 + b;
+            if (oy >= Ho2 || ox >= Wo2) continue;
+            f32x4 v = y[ay];
+            v.x = __fadd_rn(v.x, pb.x);
+            v.y = __fadd_rn(v.y, pb.y);
+            v.z = __fadd_rn(v.z, pb.z);
+            v.w = __fadd_rn(v.w, pb.w);
+            if (a.tail2.act == ACT_RELU) {
+              v.x = fmaxf(v.x, 0.f);
+              v.y = fmaxf(v.y, 0.f);
+              v.z = fmaxf(v.z, 0.f);
+              v.w = fmaxf(v.w, 0.f);
+            }
+            *reinterpret_cast<f32x4*>(a.tail2_out + ((size_t)(nimg * Ho2 + oy) * Wo2 + ox) * C2 + pcb * 16 + lg * 4) = v;
+          }
+        }
+        stamp(CH_TAIL_TS + 4);
+        stamp4(CH_W4_TAIL + 2);
+      } else {
       // ---- decode_2: conv3x3_kernel<MODE_T2, 64, 32> on T3; wave w owns input rows 2w, 2w + 1
       // (16 positions each) x both 16-channel output blocks x the four phases ----
       constexpr int C2 = 32;
@@ -925,6 +1025,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
       store2(0, CH_D2_EARLY != 0 ? 1 : 4);
       stamp(CH_TAIL_TS + 4);
       stamp4(CH_W4_TAIL + 2);
+      }
     } else {
     // + bias, act (conv3x3_kernel's epilogue), 16-byte f32 stores of the 16x16 output tile
     if (oy0 + dry < H && ox0 + drx < W) {

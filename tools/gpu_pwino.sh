@@ -13,7 +13,7 @@ T=$R/tf_image_compression_amd/tune
 for part in "$@"; do
   case $part in
     tests) step pwtests_$TAG 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu \
-             tests/test_gpu_pwino.py ;;
+             tests/test_gpu_pwino.py tests/test_gpu_chain.py ;;
     probe) step pwprobe0_$TAG 300 python tools/layer_probe.py 0 32 'opt:s2_form=0' 'opt:s2_form=1' \
              'opt:s1_form=0,opt:s2_form=0' 'opt:s1_form=0,opt:s2_form=1' &&
            step pwprobe3_$TAG 400 python tools/layer_probe.py 3 128 'opt:s2_form=0' 'opt:s2_form=1' ;;
