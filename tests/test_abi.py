@@ -304,8 +304,15 @@ def test_bench_direct_equiv_mixed_form_chain():
     bench.winograd_note(roof, dom_k, fam, 32, dom_ms)
     assert abs(direct * 32 / 1e9 - (3.623 + 4.831)) < 0.01
     assert abs(roof["direct_equiv_tflops"] - 64.3) < 0.1, roof
-    assert "direct form for the stride-2" in roof["flop_form"]
+    assert "stride-2 / transposed ones in their own form" in roof["flop_form"]
     assert abs(roof["frac"] - 0.2465) < 0.002  # executed FLOPs over the peak, unchanged
+    # the decoder chain with its decode_2 in the polyphase form (HT bit 8): that layer counts
+    # 25/36 of its direct FLOPs, the rest as before
+    kernels[d0] = "wino_chain_kernel<1,0,2,14>"
+    groups14, _ = bench.kernel_groups(None, 0, 256, ms, kernels)
+    fam14 = bench.kernel_families(groups14, kernels, names)["wino_chain_kernel"]
+    assert abs(fam14["direct_flops"] - fam["direct_flops"]) < 1e-6
+    assert abs((fam["flops"] - fam14["flops"]) * 2 - work[d2][1] * (1 - bench.PWINO_FRAC)) < 1e-3
     # a pure Winograd group keeps the plain 16/36 conversion
     g = {"flops": 10e9 * bench.WINO_FRAC, "direct_flops": 10e9}
     r = {}
