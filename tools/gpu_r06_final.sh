@@ -8,6 +8,10 @@
 #                                            round-5 library + its shipped tuning (libtic_r05.so,
 #                                            tools/tune_ab/model{0,3}_r05.json) and the current
 #                                            ones, separate processes, model_0 then model_3
+#   bash tools/gpu_r06_final.sh <tag> retune  a second fresh model_0 / model_3 tuning (compared
+#                                            with the shipped files: the tuner's reproducibility)
+#   bash tools/gpu_r06_final.sh <tag> exp     one-lane layer times of model_3 with the polyphase
+#                                            form in libtic_exp.so (tools/experiments/pwino_nnb2.patch)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1
 PART=$2
@@ -50,4 +54,14 @@ if [ "$PART" = abdrv ]; then
       echo "m3 $v $i $(grep -o '"value": [0-9.]*' $O/abdrv_${TAG}_m3_${v}_$i.log | head -1)"
     done
   done
+fi
+if [ "$PART" = retune ]; then
+  mkdir -p $O/tune_$TAG
+  step retune_m0_$TAG 600 python bench.py --tune-cache none --tune-save $O/tune_$TAG --no-cpu-baseline
+  step retune_m3_$TAG 900 python bench.py --model 3 --batch 256 --tune-cache none --tune-save $O/tune_$TAG \
+    --no-cpu-baseline --steps 20 --warmup 5
+fi
+if [ "$PART" = exp ]; then
+  TIC_LIB=$R/tf_image_compression_amd/libtic_exp.so step exp3_$TAG 400 python tools/layer_probe.py 3 128 \
+    'opt:s2_form=0' 'opt:s2_form=1'
 fi
