@@ -118,7 +118,7 @@ int tic_rmbe_device(tic_handle* h, const float* d_windows, int n, float* d_out);
  * for the 64->64 res-block convs, other layers falling back to 1; -1 the model's default: 2 for
  * model_3 and the rmbe net, 1 otherwise; env TIC_S1_FORM=direct|wino|wino4), "s2_form" (standalone
  * stride-2 / transposed layers: 0 direct, 1 polyphase Winograd — layers a fused kernel could run
- * keep the direct form; -1 the model's default: 1 for models 0/1, 0 otherwise; env TIC_S2_FORM=direct|pwino), "decouple" (lanes fork from the
+ * keep the direct form; -1 the model's default: 1 for models 0, 1 and 3 (80-channel layers direct), 0 otherwise; env TIC_S2_FORM=direct|pwino), "decouple" (lanes fork from the
  * handle stream only when a call's device byte ranges or earlier non-lane work require it;
  * default 1), "mark_layer" (see tic_mark_durations). */
 int tic_set_option(tic_handle* h, const char* key, int value);

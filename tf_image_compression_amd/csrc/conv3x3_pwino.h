@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(64 * (COUT / 16) * NNB) conv3x3_pwino_kernel(c
   // stride 2: the staged rows stream in the order 2, 0, 4, 1, 3, one per point row (xi = 1,
   // 0, 2, 3, 4; row 2 kept for xi 0 and 2); transpose: xi in order
   constexpr int XO[5] = {MODE == MODE_S2 ? 1 : 0, MODE == MODE_S2 ? 0 : 1, 2, 3, 4};
-  constexpr int NSTEP = 25 * KC, PF = 8;
+  // a point row's five U fragments arrive one row (5 steps) ahead, in a ring of two rows
+  constexpr int NSTEP = 25 * KC, PF = 5, RING = PF + 5;
   const __amdgpu_buffer_rsrc_t wrs = weight_rsrc(a.wp, 25 * CIN * COUT * 4);
   const int wlb = (lg * COUT + cb * 16 + li) * 16;
   auto wglob = [&](int s) -> f32x4 {
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(64 * (COUT / 16) * NNB) conv3x3_pwino_kernel(c
     const int p = 5 * XO[q] + nu;
     return weight_frag(wrs, wlb, ((p * KC + kc) * 4 * COUT * 4) * 4);
   };
-  f32x4 av[PF + 1];
+  f32x4 av[RING];
 #pragma unroll
   for (int p = 0; p < PF; ++p) av[p] = wglob(p);
 
@@ -206,15 +207,21 @@ __global__ void __launch_bounds__(64 * (COUT / 16) * NNB) conv3x3_pwino_kernel(c
 #pragma unroll
   for (int p = 0; p < 25; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
   // the five point GEMMs of point row xi at chunk kc and row step q (weights step 5 q + nu)
+  // (t outer, nu inner: consecutive MFMAs feed five different accumulators, so no MFMA waits
+  // for the one before it; each point still sums over t in order — the same bits)
   auto row_mfma = [&](int q, int xi, const f32x4 (&V)[5]) {
+    f32x4 u[5];
+#pragma unroll
+    for (int nu = 0; nu < 5; ++nu) u[nu] = av[(5 * q + nu) % RING];
 #pragma unroll
     for (int nu = 0; nu < 5; ++nu) {
-      const int s = 5 * q + nu;
-      if (s + PF < NSTEP) av[(s + PF) % (PF + 1)] = wglob(s + PF);
-      const f32x4 u = av[s % (PF + 1)];
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) acc[5 * xi + nu] = mfma4(u[tt], V[nu][tt], acc[5 * xi + nu]);
+      const int s = 5 * q + nu + PF;
+      if (s < NSTEP) av[s % RING] = wglob(s);
     }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int nu = 0; nu < 5; ++nu) acc[5 * xi + nu] = mfma4(u[nu][tt], V[nu][tt], acc[5 * xi + nu]);
   };
 
 #pragma unroll

@@ -749,18 +749,17 @@ int default_s1_form(int model_id) {
 }
 
 // Stride-2 / transposed form policy: TIC_S2_FORM=direct|pwino, else built-in (DESIGN.md §3
-// "polyphase Winograd"): the polyphase form for models 0/1, whose layers it runs (encode_2, a
-// 64x64 -> 32x32 grid of 512+ workgroups per lane, and the decode_2 behind the decoder chain's
-// tail) got faster with it (model_0 configs[1] step -1.3 / -1.8 % in two alternating A/B runs);
-// the direct form elsewhere: model_2's encode_4 / decode_4, model_3's 64- and 80-channel layers
-// and the rmbe / ch_128 layers measured slower in it (one workgroup per CU or 2.8x the weight
-// bytes per output of the direct form, profiles/ab_r06_pwino.json).
+// "polyphase Winograd"): the polyphase form for models 0/1 (encode_2 and the decode_2 behind
+// the decoder chain's tail: configs[1] step -1.8 %, profiles/ab_r06_pwino.json) and model_3
+// (encode_3 / decode_3, 64 -> 64: one lane 93.8 -> 89.5 and 92.8 -> 84.2 us; its 80-channel
+// layers keep the direct form, pwino_layer); direct for model_2 (its standalone layers are
+// 16x16 grids, slower in the form), the rmbe net and ch_128 (not measured in it).
 int default_s2_form(int model_id) {
   const char* f = getenv("TIC_S2_FORM");
   const std::string s = f ? f : "";
   if (s == "pwino") return 1;
   if (s == "direct") return 0;
-  return model_id == 0 || model_id == 1 ? 1 : 0;
+  return model_id == 0 || model_id == 1 || model_id == 3 ? 1 : 0;
 }
 
 // Last-layer formulation (conv_rgb.hip): a fixed policy, never a tuning result, because
@@ -956,6 +955,12 @@ bool pwino_layer(const tic_handle* h, int i) {
   if (i <= 0 || i >= L - 1) return false;
   const LayerDef& d = h->layers[i].def;
   if (d.kind != K_S2 && d.kind != K_T2) return false;
+  // a polyphase workgroup has one wave per 16 output channels (x tile blocks): 80 output
+  // channels (model_3's quantiser, and its dequantiser's input width) give 5-wave workgroups
+  // that load the four SIMDs unevenly — measured 2x / 1.5x slower than the direct form
+  // (profiles/ab_r06_pwino_il.json); those layers keep the direct form
+  if (d.cout % 64 != 0 && d.cout != 32) return false;
+  if (d.cin % 16 != 0 || d.cin == 80) return false;
   const bool relu = d.act == 1 && !d.residual;
   if (i == 1 && d.kind == K_S2 && relu && !(!h->rmbe() && h->n_enc == 2) &&
       ((d.cin == 32 && d.cout == 32) || (d.cin == 16 && d.cout == 32) || (d.cin == 32 && d.cout == 64)))

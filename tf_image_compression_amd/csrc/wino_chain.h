@@ -841,7 +841,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
         // reading T3 positions (2ty + r, 2tx + j), r, j = 0..2 (row / column 0: the halo); wave w
         // owns output-channel block w & 1 and tile rows 2 (w >> 1) .. + 1 (lane li: tile
         // (2 (w >> 1) + li / 8, li % 8)), all 25 points: 400 MFMAs per wave instead of 576 ----
-        constexpr int C2 = 32, PPF = 8, PSTEP = 25 * KC;
+        constexpr int C2 = 32, PPF = 5, PRING = PPF + 5, PSTEP = 25 * KC;
         const int pcb = wv & 1, pty = 2 * (wv >> 1) + (li >> 3), ptx = li & 7;
         const __amdgpu_buffer_rsrc_t w2s =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.tail2.wu), (short)0, 25 * C * C2 * 4, 0x00020000);
@@ -851,7 +851,7 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
                                                                 ((p * KC + kc) * 4 * C2 * 4) * 4, 0);
           return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
         };
-        f32x4 pav[PPF + 1];
+        f32x4 pav[PRING];
 #pragma unroll
         for (int p = 0; p < PPF; ++p) pav[p] = pwglob(p);
         const f32x4 pb = *reinterpret_cast<const f32x4*>(a.tail2.bias + pcb * 16 + lg * 4);
@@ -878,14 +878,18 @@ __global__ void __launch_bounds__(256 * WH, WH == 1 ? 2 : 1) wino_chain_kernel(c
 #pragma unroll
             for (int j = 0; j < 3; ++j) r[j] = pw_row_t2(xi, d[0][j], d[1][j], d[2][j]);
             pw_bt<MODE_T2>(r, V);
+            // U one point row ahead; t outer, nu inner (no MFMA waits for the one before it)
+            const int s0 = 25 * kc + 5 * xi;
+            f32x4 u[5];
 #pragma unroll
-            for (int nu = 0; nu < 5; ++nu) {
-              const int s = 25 * kc + 5 * xi + nu;
-              if (s + PPF < PSTEP) pav[(s + PPF) % (PPF + 1)] = pwglob(s + PPF);
-              const f32x4 u = pav[s % (PPF + 1)];
+            for (int nu = 0; nu < 5; ++nu) u[nu] = pav[(s0 + nu) % PRING];
 #pragma unroll
-              for (int tt = 0; tt < 4; ++tt) pacc[5 * xi + nu] = mfma4(u[tt], V[nu][tt], pacc[5 * xi + nu]);
-            }
+            for (int nu = 0; nu < 5; ++nu)
+              if (s0 + nu + PPF < PSTEP) pav[(s0 + nu + PPF) % PRING] = pwglob(s0 + nu + PPF);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+              for (int nu = 0; nu < 5; ++nu) pacc[5 * xi + nu] = mfma4(u[nu][tt], V[nu][tt], pacc[5 * xi + nu]);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
