@@ -10,6 +10,8 @@
 #                                            ones, separate processes, model_0 then model_3
 #   bash tools/gpu_r06_final.sh <tag> retune  a second fresh model_0 / model_3 tuning (compared
 #                                            with the shipped files: the tuner's reproducibility)
+#   bash tools/gpu_r06_final.sh <tag> extra   the driver's command twice more, SQ counters of the
+#                                            model_3 step, rocprofv3 stats of configs[4]
 #   bash tools/gpu_r06_final.sh <tag> exp     one-lane layer times of model_3 with the polyphase
 #                                            form in libtic_exp.so (tools/experiments/pwino_nnb2.patch)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -64,4 +66,13 @@ fi
 if [ "$PART" = exp ]; then
   TIC_LIB=$R/tf_image_compression_amd/libtic_exp.so step exp3_$TAG 400 python tools/layer_probe.py 3 128 \
     'opt:s2_form=0' 'opt:s2_form=1'
+fi
+if [ "$PART" = extra ]; then
+  step xdrv1_$TAG 300 python bench.py --gpus 1 --steps 20 --warmup 5
+  step xdrv2_$TAG 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+  step kc3_$TAG 900 bash tools/kcounters.sh m3_$TAG $T/model3_p256_b256_s2.json --model 3 --batch 256
+  cd /tmp && export TMPDIR=/tmp
+  step prof_img_$TAG 400 rocprofv3 --kernel-trace --stats -d $O/prof_img_$TAG -o p -- python3 $R/bench.py \
+    --no-cpu-baseline --workload image4k --steps 10 --warmup 2
+  cd $R
 fi
